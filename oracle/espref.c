@@ -1,0 +1,991 @@
+/*
+ * espref.c — CPU restatement of FreeBSD's ESP bulk-crypto path (see espref.h).
+ *
+ * TEST INFRASTRUCTURE ONLY (parity oracle + "port" CPU baseline).  Not part of
+ * the product; the product never links it.
+ *
+ * Written from the reference's algorithms, not copied: the AES tables are
+ * generated from the field arithmetic instead of the constant arrays of
+ * rijndael-alg-fst.c:57-733, and the GHASH reduction table is derived from
+ * the polynomial rather than taken from gfmult.c:129.  The per-request
+ * structure (context copy per op, 16-byte GHASH updates, verify-then-decrypt)
+ * deliberately mirrors cryptosoft.c so that its timing is "cryptosoft-shaped".
+ */
+#include "espref.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ------------------------------------------------------------------------ */
+/* Byte helpers (GETU32/PUTU32 of rijndael_local.h, be64dec/enc of gfmult.h) */
+
+static inline uint32_t ld_be32(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
+	    ((uint32_t)p[2] << 8) | p[3];
+}
+
+static inline void st_be32(uint8_t *p, uint32_t v)
+{
+	p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v;
+}
+
+static inline uint64_t ld_be64(const uint8_t *p)
+{
+	return ((uint64_t)ld_be32(p) << 32) | ld_be32(p + 4);
+}
+
+static inline void st_be64(uint8_t *p, uint64_t v)
+{
+	st_be32(p, (uint32_t)(v >> 32));
+	st_be32(p + 4, (uint32_t)v);
+}
+
+static inline uint32_t ror32(uint32_t v, int n)
+{
+	return n ? (v >> n) | (v << (32 - n)) : v;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Generated tables                                                          */
+
+static uint8_t SBOX[256], ISBOX[256];
+static uint32_t TE[4][256], TD[4][256];   /* Te0..Te3 / Td0..Td3 */
+static uint16_t GHRED[16];                /* gfmult.c:129 reduction[] */
+static pthread_once_t tables_once = PTHREAD_ONCE_INIT;
+
+static uint8_t xtime8(uint8_t a)
+{
+	return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+}
+
+static uint8_t gmul8(uint8_t a, uint8_t b)
+{
+	uint8_t r = 0;
+
+	while (b) {
+		if (b & 1)
+			r ^= a;
+		a = xtime8(a);
+		b >>= 1;
+	}
+	return r;
+}
+
+static uint8_t rotl8(uint8_t v, int n)
+{
+	return (uint8_t)((v << n) | (v >> (8 - n)));
+}
+
+static void gen_tables(void)
+{
+	/* S-box: inverse in GF(2^8) mod x^8+x^4+x^3+x+1, then the affine map. */
+	for (int x = 0; x < 256; x++) {
+		uint8_t inv = 0;
+		if (x != 0)
+			for (int y = 1; y < 256; y++)
+				if (gmul8((uint8_t)x, (uint8_t)y) == 1) {
+					inv = (uint8_t)y;
+					break;
+				}
+		uint8_t s = inv ^ rotl8(inv, 1) ^ rotl8(inv, 2) ^ rotl8(inv, 3) ^
+		    rotl8(inv, 4) ^ 0x63;
+		SBOX[x] = s;
+		ISBOX[s] = (uint8_t)x;
+	}
+	/* Te0[x] = S[x].[02,01,01,03], Td0[x] = Si[x].[0e,09,0d,0b]
+	 * (rijndael-alg-fst.c:43-55); TeN/TdN are byte rotations. */
+	for (int x = 0; x < 256; x++) {
+		uint8_t s = SBOX[x], si = ISBOX[x];
+		uint32_t te = ((uint32_t)gmul8(s, 2) << 24) | ((uint32_t)s << 16) |
+		    ((uint32_t)s << 8) | gmul8(s, 3);
+		uint32_t td = ((uint32_t)gmul8(si, 14) << 24) |
+		    ((uint32_t)gmul8(si, 9) << 16) | ((uint32_t)gmul8(si, 13) << 8) |
+		    gmul8(si, 11);
+		for (int k = 0; k < 4; k++) {
+			TE[k][x] = ror32(te, 8 * k);
+			TD[k][x] = ror32(td, 8 * k);
+		}
+	}
+	/*
+	 * GHASH x^4 reduction (gfmult.c:125-132): bit j of the four bits shifted
+	 * out of v[1] has degree 127-j; times x^4 it becomes R*x^(3-j) with
+	 * R = x^7+x^2+x+1, i.e. 0xE1 in the reflected top byte.
+	 */
+	for (int r = 0; r < 16; r++) {
+		uint16_t v = 0;
+		for (int j = 0; j < 4; j++)
+			if (r & (1 << j))
+				v ^= (uint16_t)(0xE100 >> (3 - j));
+		GHRED[r] = v;
+	}
+}
+
+static void init_tables(void)
+{
+	pthread_once(&tables_once, gen_tables);
+}
+
+/* ------------------------------------------------------------------------ */
+/* AES (rijndael-alg-fst.c)                                                  */
+
+static uint32_t subword(uint32_t w)
+{
+	return ((uint32_t)SBOX[w >> 24] << 24) | ((uint32_t)SBOX[(w >> 16) & 0xff] << 16) |
+	    ((uint32_t)SBOX[(w >> 8) & 0xff] << 8) | SBOX[w & 0xff];
+}
+
+/* rijndaelKeySetupEnc, rijndael-alg-fst.c:735-821 (FIPS-197 5.2, any Nk). */
+int oref_aes_setkey_enc(uint32_t rk[60], const uint8_t *key, int keybits)
+{
+	int nk = keybits / 32, nr, i;
+	uint32_t rcon = 0x01000000;
+
+	init_tables();
+	if (keybits != 128 && keybits != 192 && keybits != 256)
+		return 0;
+	nr = nk + 6;
+	for (i = 0; i < nk; i++)
+		rk[i] = ld_be32(key + 4 * i);
+	for (; i < 4 * (nr + 1); i++) {
+		uint32_t t = rk[i - 1];
+		if (i % nk == 0) {
+			t = subword((t << 8) | (t >> 24)) ^ rcon;
+			rcon = (uint32_t)xtime8((uint8_t)(rcon >> 24)) << 24;
+		} else if (nk > 6 && i % nk == 4) {
+			t = subword(t);
+		}
+		rk[i] = rk[i - nk] ^ t;
+	}
+	return nr;
+}
+
+static uint32_t inv_mixcol(uint32_t w)
+{
+	uint8_t a0 = w >> 24, a1 = w >> 16, a2 = w >> 8, a3 = w;
+	uint8_t b0 = gmul8(a0, 14) ^ gmul8(a1, 11) ^ gmul8(a2, 13) ^ gmul8(a3, 9);
+	uint8_t b1 = gmul8(a0, 9) ^ gmul8(a1, 14) ^ gmul8(a2, 11) ^ gmul8(a3, 13);
+	uint8_t b2 = gmul8(a0, 13) ^ gmul8(a1, 9) ^ gmul8(a2, 14) ^ gmul8(a3, 11);
+	uint8_t b3 = gmul8(a0, 11) ^ gmul8(a1, 13) ^ gmul8(a2, 9) ^ gmul8(a3, 14);
+	return ((uint32_t)b0 << 24) | ((uint32_t)b1 << 16) | ((uint32_t)b2 << 8) | b3;
+}
+
+/* rijndaelKeySetupDec, rijndael-alg-fst.c:823-861: reverse the round order,
+ * InvMixColumns on every round key but the first and last. */
+int oref_aes_setkey_dec(uint32_t rk[60], const uint8_t *key, int keybits)
+{
+	int nr = oref_aes_setkey_enc(rk, key, keybits);
+
+	for (int i = 0, j = 4 * nr; i < j; i += 4, j -= 4)
+		for (int k = 0; k < 4; k++) {
+			uint32_t t = rk[i + k];
+			rk[i + k] = rk[j + k];
+			rk[j + k] = t;
+		}
+	for (int i = 4; i < 4 * nr; i++)
+		rk[i] = inv_mixcol(rk[i]);
+	return nr;
+}
+
+/* rijndaelEncrypt, rijndael-alg-fst.c:863-1042 */
+void oref_aes_encrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16])
+{
+	uint32_t s[4], t[4];
+
+	for (int c = 0; c < 4; c++)
+		s[c] = ld_be32(in + 4 * c) ^ rk[c];
+	for (int r = 1; r < nr; r++) {
+		for (int c = 0; c < 4; c++)
+			t[c] = TE[0][s[c] >> 24] ^ TE[1][(s[(c + 1) & 3] >> 16) & 0xff] ^
+			    TE[2][(s[(c + 2) & 3] >> 8) & 0xff] ^ TE[3][s[(c + 3) & 3] & 0xff] ^
+			    rk[4 * r + c];
+		memcpy(s, t, sizeof(s));
+	}
+	for (int c = 0; c < 4; c++) {
+		uint32_t v = ((uint32_t)SBOX[s[c] >> 24] << 24) |
+		    ((uint32_t)SBOX[(s[(c + 1) & 3] >> 16) & 0xff] << 16) |
+		    ((uint32_t)SBOX[(s[(c + 2) & 3] >> 8) & 0xff] << 8) |
+		    SBOX[s[(c + 3) & 3] & 0xff];
+		st_be32(out + 4 * c, v ^ rk[4 * nr + c]);
+	}
+}
+
+/* rijndaelDecrypt, rijndael-alg-fst.c:1044-1222 (equivalent inverse cipher) */
+void oref_aes_decrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16])
+{
+	uint32_t s[4], t[4];
+
+	for (int c = 0; c < 4; c++)
+		s[c] = ld_be32(in + 4 * c) ^ rk[c];
+	for (int r = 1; r < nr; r++) {
+		for (int c = 0; c < 4; c++)
+			t[c] = TD[0][s[c] >> 24] ^ TD[1][(s[(c + 3) & 3] >> 16) & 0xff] ^
+			    TD[2][(s[(c + 2) & 3] >> 8) & 0xff] ^ TD[3][s[(c + 1) & 3] & 0xff] ^
+			    rk[4 * r + c];
+		memcpy(s, t, sizeof(s));
+	}
+	for (int c = 0; c < 4; c++) {
+		uint32_t v = ((uint32_t)ISBOX[s[c] >> 24] << 24) |
+		    ((uint32_t)ISBOX[(s[(c + 3) & 3] >> 16) & 0xff] << 16) |
+		    ((uint32_t)ISBOX[(s[(c + 2) & 3] >> 8) & 0xff] << 8) |
+		    ISBOX[s[(c + 1) & 3] & 0xff];
+		st_be32(out + 4 * c, v ^ rk[4 * nr + c]);
+	}
+}
+
+/* ------------------------------------------------------------------------ */
+/* GHASH (gfmult.c / gfmult.h): bit-reflected GF(2^128), v[0] = bytes 0-7   */
+/* big-endian, 4-bit tables with bit-reversed indexes striped in 4 columns. */
+
+typedef struct { uint64_t v[2]; } gf128;
+struct gftab { uint32_t a[16], b[16], c[16], d[16]; };   /* gfmult.h:56-61 */
+struct gftab4 { struct gftab t[4]; };                       /* h, h^2, h^3, h^4 */
+
+static const uint8_t NIBREV[16] = {   /* bit reversal of a nibble */
+	0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15 };
+
+static inline gf128 gf_read(const uint8_t *b)
+{
+	gf128 r = { { ld_be64(b), ld_be64(b + 8) } };
+	return r;
+}
+
+static inline void gf_write(gf128 x, uint8_t *b)
+{
+	st_be64(b, x.v[0]);
+	st_be64(b + 8, x.v[1]);
+}
+
+static inline gf128 gf_add(gf128 a, gf128 b)
+{
+	a.v[0] ^= b.v[0];
+	a.v[1] ^= b.v[1];
+	return a;
+}
+
+/* multiply by alpha (x): right shift with 0xE1 reduction, gfmult.c:44-55 */
+static gf128 gf_mulalpha(gf128 v)
+{
+	uint64_t carry = v.v[1] & 1;
+
+	v.v[1] = (v.v[1] >> 1) | (v.v[0] << 63);
+	v.v[0] = (v.v[0] >> 1) ^ (carry ? (uint64_t)0xE1 << 56 : 0);
+	return v;
+}
+
+/* gf128_genmultable, gfmult.c:62-84 */
+static void gf_genmultable(gf128 h, struct gftab *t)
+{
+	gf128 m[16];
+
+	m[0].v[0] = m[0].v[1] = 0;
+	m[1] = h;
+	for (int i = 2; i < 16; i += 2) {
+		m[i] = gf_mulalpha(m[i / 2]);
+		m[i + 1] = gf_add(m[i], h);
+	}
+	for (int i = 0; i < 16; i++) {
+		t->a[NIBREV[i]] = (uint32_t)(m[i].v[0] >> 32);
+		t->b[NIBREV[i]] = (uint32_t)m[i].v[0];
+		t->c[NIBREV[i]] = (uint32_t)(m[i].v[1] >> 32);
+		t->d[NIBREV[i]] = (uint32_t)m[i].v[1];
+	}
+}
+
+static inline gf128 gf_row(const struct gftab *t, unsigned n)   /* readrow, :111-122 */
+{
+	gf128 r;
+
+	n &= 15;
+	r.v[0] = ((uint64_t)t->a[n] << 32) | t->b[n];
+	r.v[1] = ((uint64_t)t->c[n] << 32) | t->d[n];
+	return r;
+}
+
+static inline gf128 gf_shift4(gf128 x)   /* x * alpha^4 */
+{
+	unsigned red = x.v[1] & 15;
+
+	x.v[1] = (x.v[1] >> 4) | (x.v[0] << 60);
+	x.v[0] = (x.v[0] >> 4) ^ ((uint64_t)GHRED[red] << 48);
+	return x;
+}
+
+/* gfmultword, gfmult.c:138-162: Horner over the 16 nibbles of one word,
+ * highest-degree nibble (the low bits) first. */
+static gf128 gf_multword(uint64_t w, gf128 x, const struct gftab *t)
+{
+	for (int i = 0; i < 16; i++, w >>= 4) {
+		gf128 row = gf_row(t, (unsigned)w);
+		x = gf_add(gf_shift4(x), row);
+	}
+	return x;
+}
+
+static gf128 gf_mul(gf128 v, const struct gftab *t)   /* gf128_mul, :219-229 */
+{
+	gf128 r = { { 0, 0 } };
+
+	r = gf_multword(v.v[1], r, t);
+	return gf_multword(v.v[0], r, t);
+}
+
+/* gfmultword4, gfmult.c:174-216: four words against h^4,h^3,h^2,h */
+static gf128 gf_multword4(uint64_t wa, uint64_t wb, uint64_t wc, uint64_t wd,
+    gf128 x, const struct gftab4 *t)
+{
+	for (int i = 0; i < 16; i++) {
+		gf128 row = gf_add(gf_row(&t->t[3], (unsigned)wa),
+		    gf_add(gf_row(&t->t[2], (unsigned)wb),
+		    gf_add(gf_row(&t->t[1], (unsigned)wc), gf_row(&t->t[0], (unsigned)wd))));
+		x = gf_add(gf_shift4(x), row);
+		wa >>= 4; wb >>= 4; wc >>= 4; wd >>= 4;
+	}
+	return x;
+}
+
+/* gf128_mul4b, gfmult.c:262-275 */
+static gf128 gf_mul4b(gf128 r, const uint8_t *v, const struct gftab4 *t)
+{
+	gf128 a = gf_add(r, gf_read(v)), b = gf_read(v + 16), c = gf_read(v + 32),
+	    d = gf_read(v + 48), x = { { 0, 0 } };
+
+	x = gf_multword4(a.v[1], b.v[1], c.v[1], d.v[1], x, t);
+	return gf_multword4(a.v[0], b.v[0], c.v[0], d.v[0], x, t);
+}
+
+/* gf128_genmultable4, gfmult.c:89-106 */
+static void gf_genmultable4(gf128 h, struct gftab4 *t)
+{
+	gf128 h2, h3, h4;
+
+	gf_genmultable(h, &t->t[0]);
+	h2 = gf_mul(h, &t->t[0]);
+	gf_genmultable(h2, &t->t[1]);
+	h3 = gf_mul(h, &t->t[1]);
+	gf_genmultable(h3, &t->t[2]);
+	h4 = gf_mul(h2, &t->t[1]);
+	gf_genmultable(h4, &t->t[3]);
+}
+
+void oref_gf128_mul(const uint8_t h[16], const uint8_t x[16], uint8_t out[16])
+{
+	struct gftab t;
+
+	init_tables();
+	gf_genmultable(gf_read(h), &t);
+	gf_write(gf_mul(gf_read(x), &t), out);
+}
+
+/* ------------------------------------------------------------------------ */
+/* AES-GMAC context (gmac.h:42-48, gmac.c:39-131)                            */
+
+struct gmac_ctx {
+	struct gftab4 tbl;
+	gf128 hash;
+	uint32_t ks[60];
+	uint8_t counter[16];
+	int rounds;
+};
+
+static void gmac_setkey(struct gmac_ctx *g, const uint8_t *key, int klen)
+{
+	static const uint8_t zero[16];
+	uint8_t hb[16];
+
+	memset(g, 0, sizeof(*g));                       /* AES_GMAC_Init */
+	g->rounds = oref_aes_setkey_enc(g->ks, key, klen * 8);
+	oref_aes_encrypt(g->ks, g->rounds, zero, hb);   /* H = E_K(0^128) */
+	gf_genmultable4(gf_read(hb), &g->tbl);
+}
+
+static void gmac_update(struct gmac_ctx *g, const uint8_t *p, unsigned len)
+{
+	gf128 v = g->hash;
+
+	while (len > 0) {
+		unsigned n;
+		if (len >= 64) {
+			n = 64;
+			v = gf_mul4b(v, p, &g->tbl);
+		} else if (len >= 16) {
+			n = 16;
+			v = gf_mul(gf_add(v, gf_read(p)), &g->tbl.t[0]);
+		} else {
+			uint8_t buf[16] = { 0 };
+			n = len;
+			memcpy(buf, p, n);
+			v = gf_mul(gf_add(v, gf_read(buf)), &g->tbl.t[0]);
+		}
+		len -= n;
+		p += n;
+	}
+	g->hash = v;
+}
+
+static void gmac_final(uint8_t tag[16], struct gmac_ctx *g)
+{
+	uint8_t e[16];
+
+	g->counter[15] = 1;                             /* J0 = IV || 0^31 || 1 */
+	oref_aes_encrypt(g->ks, g->rounds, g->counter, e);
+	gf_write(gf_add(g->hash, gf_read(e)), tag);
+}
+
+/* ------------------------------------------------------------------------ */
+/* AES-ICM in GCM mode (xform_aes_icm.c:126-194)                             */
+
+struct icm_ctx {
+	uint32_t ek[60];
+	int nr;
+	uint8_t block[16];
+};
+
+static void icm_gcm_reinit(struct icm_ctx *c, const uint8_t iv[12])
+{
+	memcpy(c->block, iv, 12);
+	c->block[12] = c->block[13] = c->block[14] = 0;
+	c->block[15] = 2;                               /* counter 1 is the tag's */
+}
+
+static void icm_crypt_last(struct icm_ctx *c, const uint8_t *in, uint8_t *out, int n)
+{
+	uint8_t ks[16];
+
+	oref_aes_encrypt(c->ek, c->nr, c->block, ks);
+	for (int i = 0; i < n; i++)
+		out[i] = in[i] ^ ks[i];
+}
+
+static void icm_crypt(struct icm_ctx *c, const uint8_t *in, uint8_t *out)
+{
+	icm_crypt_last(c, in, out, 16);
+	for (int i = 15; i >= 0; i--)                   /* full 128-bit increment */
+		if (++c->block[i])
+			break;
+}
+
+/* ------------------------------------------------------------------------ */
+/* SHA-1 (sha1.c) and HMAC (crypto.c:413-457)                                */
+
+struct sha1_ctx {
+	uint32_t h[5];
+	uint64_t nbytes;
+	uint8_t buf[64];
+	unsigned fill;
+};
+
+static void sha1_block(uint32_t h[5], const uint8_t *m)   /* sha1_step, sha1.c:94-176 */
+{
+	uint32_t w[80], a, b, c, d, e;
+
+	for (int t = 0; t < 16; t++)
+		w[t] = ld_be32(m + 4 * t);
+	for (int t = 16; t < 80; t++) {
+		uint32_t x = w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16];
+		w[t] = (x << 1) | (x >> 31);
+	}
+	a = h[0]; b = h[1]; c = h[2]; d = h[3]; e = h[4];
+	for (int t = 0; t < 80; t++) {
+		uint32_t f, k;
+		if (t < 20) {
+			f = (b & c) | (~b & d); k = 0x5a827999;
+		} else if (t < 40) {
+			f = b ^ c ^ d; k = 0x6ed9eba1;
+		} else if (t < 60) {
+			f = (b & c) | (b & d) | (c & d); k = 0x8f1bbcdc;
+		} else {
+			f = b ^ c ^ d; k = 0xca62c1d6;
+		}
+		uint32_t tmp = ((a << 5) | (a >> 27)) + f + e + w[t] + k;
+		e = d; d = c; c = (b << 30) | (b >> 2); b = a; a = tmp;
+	}
+	h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+static void sha1_init(struct sha1_ctx *s)   /* sha1_init, sha1.c:178-188 */
+{
+	static const uint32_t iv[5] = { 0x67452301, 0xefcdab89, 0x98badcfe,
+	    0x10325476, 0xc3d2e1f0 };
+	memcpy(s->h, iv, sizeof(iv));
+	s->nbytes = 0;
+	s->fill = 0;
+}
+
+static void sha1_update(struct sha1_ctx *s, const uint8_t *p, size_t n)   /* sha1_loop */
+{
+	s->nbytes += n;
+	while (n > 0) {
+		size_t k = 64 - s->fill;
+		if (k > n)
+			k = n;
+		memcpy(s->buf + s->fill, p, k);
+		s->fill += (unsigned)k;
+		p += k;
+		n -= k;
+		if (s->fill == 64) {
+			sha1_block(s->h, s->buf);
+			s->fill = 0;
+		}
+	}
+}
+
+static void sha1_final(uint8_t out[20], struct sha1_ctx *s)   /* sha1_pad + sha1_result */
+{
+	uint64_t bits = s->nbytes * 8;
+	uint8_t pad = 0x80, z = 0, lb[8];
+
+	sha1_update(s, &pad, 1);
+	while (s->fill != 56)
+		sha1_update(s, &z, 1);
+	st_be64(lb, bits);
+	sha1_update(s, lb, 8);
+	for (int i = 0; i < 5; i++)
+		st_be32(out + 4 * i, s->h[i]);
+}
+
+void oref_sha1(const uint8_t *msg, size_t len, uint8_t out[20])
+{
+	struct sha1_ctx s;
+
+	sha1_init(&s);
+	sha1_update(&s, msg, len);
+	sha1_final(out, &s);
+}
+
+/* hmac_init_pad, crypto.c:413-441 */
+static void hmac_pad(const uint8_t *key, int klen, struct sha1_ctx *s, uint8_t padval)
+{
+	uint8_t k[64];
+
+	memset(k, 0, sizeof(k));
+	if (klen > 64) {
+		oref_sha1(key, (size_t)klen, k);
+		klen = 20;
+	} else {
+		memcpy(k, key, (size_t)klen);
+	}
+	for (int i = 0; i < 64; i++)
+		k[i] ^= padval;
+	sha1_init(s);
+	sha1_update(s, k, 64);
+}
+
+void oref_hmac_sha1(const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t out[20])
+{
+	struct sha1_ctx i, o;
+	uint8_t inner[20];
+
+	hmac_pad(key, klen, &i, 0x36);
+	hmac_pad(key, klen, &o, 0x5c);
+	sha1_update(&i, msg, len);
+	sha1_final(inner, &i);
+	sha1_update(&o, inner, 20);
+	sha1_final(out, &o);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Sessions (cryptosoft.c:976-1128, 1309-1409)                               */
+
+struct oref_sa {
+	int mode, flags, mlen, klen;
+	uint8_t salt[4];
+	/* GCM: sw_ictx (AES-GMAC ctx) + sw_kschedule (ICM ctx) */
+	struct gmac_ctx gictx;
+	struct icm_ctx icm;
+	/* ETA: rijndael ctx + HMAC ipad/opad contexts */
+	uint32_t ek[60], dk[60];
+	int nr;
+	struct sha1_ctx ictx, octx;
+};
+
+oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
+    const uint8_t salt[4], const uint8_t *akey, int aklen, int mlen)
+{
+	oref_sa *sa;
+
+	init_tables();
+	if (cklen != 16 && cklen != 24 && cklen != 32)
+		return NULL;
+	sa = calloc(1, sizeof(*sa));
+	if (sa == NULL)
+		return NULL;
+	sa->mode = mode;
+	sa->flags = flags;
+	sa->klen = cklen;
+	if (mode == OREF_CSP_MODE_AEAD) {               /* swcr_setup_gcm :1087 */
+		sa->mlen = (mlen == 0) ? 16 : mlen;
+		gmac_setkey(&sa->gictx, ckey, cklen);
+		sa->icm.nr = oref_aes_setkey_enc(sa->icm.ek, ckey, cklen * 8);
+		if (salt)
+			memcpy(sa->salt, salt, 4);
+	} else if (mode == OREF_CSP_MODE_ETA) {         /* swcr_setup_cipher/auth */
+		sa->mlen = (mlen == 0) ? 20 : mlen;
+		sa->nr = oref_aes_setkey_enc(sa->ek, ckey, cklen * 8);
+		oref_aes_setkey_dec(sa->dk, ckey, cklen * 8);
+		hmac_pad(akey, aklen, &sa->ictx, 0x36);
+		hmac_pad(akey, aklen, &sa->octx, 0x5c);
+	} else {
+		free(sa);
+		return NULL;
+	}
+	return sa;
+}
+
+void oref_sa_free(oref_sa *sa)
+{
+	free(sa);
+}
+
+/* ------------------------------------------------------------------------ */
+/* swcr_gcm on a contiguous buffer (cryptosoft.c:465-645)                    */
+
+struct req {
+	uint8_t *buf;
+	const uint8_t *aad;     /* separate AAD or NULL (then aad_start) */
+	int aad_start, aad_len;
+	int payload_start, payload_len, digest_start, iv_start;
+	uint8_t iv[16];
+	uint8_t esn[4];
+	int encrypt;
+};
+
+static int swcr_gcm_c(const oref_sa *sa, struct req *r)
+{
+	struct gmac_ctx ctx;
+	struct icm_ctx icm;
+	uint8_t blk[16], tag[16], lenblk[16];
+	int resid, len;
+
+	memcpy(&ctx, &sa->gictx, sizeof(ctx));          /* bcopy(sw_ictx) :485 */
+	memcpy(&icm, &sa->icm, sizeof(icm));
+	memcpy(ctx.counter, r->iv, 12);                 /* AES_GMAC_Reinit */
+
+	if (r->aad != NULL) {                           /* :505-515 */
+		len = r->aad_len & ~15;
+		if (len)
+			gmac_update(&ctx, r->aad, (unsigned)len);
+		if (r->aad_len != len) {
+			memset(blk, 0, 16);
+			memcpy(blk, r->aad + len, (size_t)(r->aad_len - len));
+			gmac_update(&ctx, blk, 16);
+		}
+	} else {                                        /* :517-537 */
+		const uint8_t *p = r->buf + r->aad_start;
+		len = r->aad_len & ~15;
+		if (len)
+			gmac_update(&ctx, p, (unsigned)len);
+		if (r->aad_len != len) {
+			memset(blk, 0, 16);
+			memcpy(blk, p + len, (size_t)(r->aad_len - len));
+			gmac_update(&ctx, blk, 16);
+		}
+	}
+
+	icm_gcm_reinit(&icm, r->iv);                    /* :540 */
+	uint8_t *p = r->buf + r->payload_start;
+	for (resid = r->payload_len; resid >= 16; resid -= 16, p += 16) {   /* :550-572 */
+		if (r->encrypt) {
+			icm_crypt(&icm, p, p);
+			gmac_update(&ctx, p, 16);
+		} else {
+			gmac_update(&ctx, p, 16);
+		}
+	}
+	if (resid > 0) {                                /* :573-580 */
+		memcpy(blk, p, (size_t)resid);
+		if (r->encrypt) {
+			icm_crypt_last(&icm, blk, blk, resid);
+			memcpy(p, blk, (size_t)resid);
+		}
+		gmac_update(&ctx, blk, (unsigned)resid);
+	}
+	memset(lenblk, 0, 16);                          /* :583-588 */
+	st_be32(lenblk + 4, (uint32_t)r->aad_len * 8);
+	st_be32(lenblk + 12, (uint32_t)r->payload_len * 8);
+	gmac_update(&ctx, lenblk, 16);
+	gmac_final(tag, &ctx);
+
+	if (!r->encrypt) {                              /* :593-633 */
+		uint8_t diff = 0;
+		for (int i = 0; i < sa->mlen; i++)
+			diff |= tag[i] ^ r->buf[r->digest_start + i];
+		if (diff != 0)
+			return EBADMSG;
+		p = r->buf + r->payload_start;
+		for (resid = r->payload_len; resid > 16; resid -= 16, p += 16)
+			icm_crypt(&icm, p, p);
+		if (resid > 0)
+			icm_crypt_last(&icm, p, p, resid);
+	} else {
+		memcpy(r->buf + r->digest_start, tag, (size_t)sa->mlen);   /* :636 */
+	}
+	return 0;
+}
+
+/* swcr_encdec for AES-CBC on a contiguous buffer (cryptosoft.c:101-284) */
+static int swcr_encdec_cbc(const oref_sa *sa, struct req *r)
+{
+	uint8_t iv[16], niv[16];
+	uint8_t *p = r->buf + r->payload_start;
+
+	if (r->payload_len % 16)
+		return EINVAL;
+	memcpy(iv, r->buf + r->iv_start, 16);           /* crypto_read_iv */
+	for (int resid = r->payload_len; resid >= 16; resid -= 16, p += 16) {
+		if (r->encrypt) {
+			for (int i = 0; i < 16; i++)
+				p[i] ^= iv[i];
+			oref_aes_encrypt(sa->ek, sa->nr, p, p);
+			memcpy(iv, p, 16);
+		} else {
+			memcpy(niv, p, 16);             /* keep C_i for the next block */
+			oref_aes_decrypt(sa->dk, sa->nr, p, p);
+			for (int i = 0; i < 16; i++)
+				p[i] ^= iv[i];
+			memcpy(iv, niv, 16);
+		}
+	}
+	return 0;
+}
+
+/* swcr_authcompute for HMAC-SHA1 (cryptosoft.c:317-382) */
+static int swcr_authcompute_c(const oref_sa *sa, struct req *r)
+{
+	struct sha1_ctx ctx;
+	uint8_t a[20];
+
+	memcpy(&ctx, &sa->ictx, sizeof(ctx));
+	sha1_update(&ctx, r->buf + r->aad_start, (size_t)r->aad_len);
+	sha1_update(&ctx, r->buf + r->payload_start, (size_t)r->payload_len);
+	if (sa->flags & OREF_CSP_F_ESN)
+		sha1_update(&ctx, r->esn, 4);
+	sha1_final(a, &ctx);
+	memcpy(&ctx, &sa->octx, sizeof(ctx));
+	sha1_update(&ctx, a, 20);
+	sha1_final(a, &ctx);
+	if (!r->encrypt) {
+		uint8_t diff = 0;
+		for (int i = 0; i < sa->mlen; i++)
+			diff |= a[i] ^ r->buf[r->digest_start + i];
+		return diff ? EBADMSG : 0;
+	}
+	memcpy(r->buf + r->digest_start, a, (size_t)sa->mlen);
+	return 0;
+}
+
+static int swcr_eta_c(const oref_sa *sa, struct req *r)   /* cryptosoft.c:874-888 */
+{
+	int e;
+
+	if (r->encrypt) {
+		e = swcr_encdec_cbc(sa, r);
+		return e ? e : swcr_authcompute_c(sa, r);
+	}
+	e = swcr_authcompute_c(sa, r);
+	return e ? e : swcr_encdec_cbc(sa, r);
+}
+
+/* Build the request as esp_input does (xform_esp.c:296-461, skip = 0) and
+ * as esp_output does for the encrypt direction (xform_esp.c:673-961). */
+static int esp_process(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi, int encrypt)
+{
+	struct req r;
+	uint8_t aadbuf[12];
+	int gcm = (sa->mode == OREF_CSP_MODE_AEAD);
+	int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen;
+	int alen = gcm ? 16 : 12;                       /* xform_ah_authsize */
+	int plen = len - hlen - alen;
+
+	if ((len & 3) || plen <= 0 || (!gcm && (plen & 15)))   /* :279-324 */
+		return EINVAL;
+	memset(&r, 0, sizeof(r));
+	r.buf = esp;
+	r.encrypt = encrypt;
+	r.payload_start = hlen;
+	r.payload_len = plen;
+	r.digest_start = len - alen;
+	st_be32(r.esn, esn_hi);                         /* seqh = htonl(seqh) */
+	if (gcm) {
+		r.aad_len = 8;                          /* RFC 4106: SPI + SN */
+		if (sa->flags & OREF_CSP_F_SEPARATE_AAD) {   /* :375-397 */
+			memcpy(aadbuf, esp, 4);
+			memcpy(aadbuf + 4, r.esn, 4);
+			memcpy(aadbuf + 8, esp + 4, 4);
+			r.aad = aadbuf;
+			r.aad_len = 12;
+		}
+		memcpy(r.iv, sa->salt, 4);              /* :453-455 */
+		memcpy(r.iv + 4, esp + 8, 8);
+		return swcr_gcm_c(sa, &r);
+	}
+	r.aad_start = 0;
+	r.aad_len = hlen;                               /* :369 */
+	r.iv_start = hlen - ivlen;                      /* :460-461 */
+	return swcr_eta_c(sa, &r);
+}
+
+int oref_esp_decrypt(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi)
+{
+	return esp_process(sa, esp, len, esn_hi, 0);
+}
+
+int oref_esp_encrypt(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi)
+{
+	return esp_process(sa, esp, len, esn_hi, 1);
+}
+
+int oref_gcm(const uint8_t *key, int klen, const uint8_t iv[12],
+    const uint8_t *aad, int aadlen, uint8_t *data, int len,
+    uint8_t *tag, int mlen, int encrypt)
+{
+	oref_sa *sa = oref_sa_new(OREF_CSP_MODE_AEAD, 0, key, klen, NULL, NULL, 0, mlen);
+	struct req r;
+	uint8_t *buf;
+	int e;
+
+	if (sa == NULL)
+		return EINVAL;
+	/* contiguous [data | tag] so digest_start addresses the tag */
+	buf = malloc((size_t)len + 16);
+	memcpy(buf, data, (size_t)len);
+	memcpy(buf + len, tag, 16);
+	memset(&r, 0, sizeof(r));
+	r.buf = buf;
+	r.aad = aadlen ? aad : (const uint8_t *)"";
+	r.aad_len = aadlen;
+	r.payload_start = 0;
+	r.payload_len = len;
+	r.digest_start = len;
+	r.encrypt = encrypt;
+	memcpy(r.iv, iv, 12);
+	e = swcr_gcm_c(sa, &r);
+	if (e == 0) {
+		memcpy(data, buf, (size_t)len);
+		if (encrypt)
+			memcpy(tag, buf + len, (size_t)sa->mlen);
+	}
+	free(buf);
+	oref_sa_free(sa);
+	return e;
+}
+
+/* Generic AES-CBC + HMAC-SHA1 EtA (swcr_eta) on [aad | payload | digest]. */
+int oref_eta(const uint8_t *ckey, int cklen, const uint8_t *akey, int aklen,
+    const uint8_t iv[16], const uint8_t *aad, int aadlen, uint8_t *data, int len,
+    uint8_t *digest, int mlen, int encrypt)
+{
+	oref_sa *sa = oref_sa_new(OREF_CSP_MODE_ETA, 0, ckey, cklen, NULL, akey, aklen, mlen);
+	struct req r;
+	uint8_t *buf;
+	int e;
+
+	if (sa == NULL)
+		return EINVAL;
+	buf = malloc((size_t)(16 + aadlen + len + 20));
+	memcpy(buf, iv, 16);
+	memcpy(buf + 16, aad, (size_t)aadlen);
+	memcpy(buf + 16 + aadlen, data, (size_t)len);
+	memcpy(buf + 16 + aadlen + len, digest, 20);
+	memset(&r, 0, sizeof(r));
+	r.buf = buf;
+	r.iv_start = 0;
+	r.aad_start = 16;
+	r.aad_len = aadlen;
+	r.payload_start = 16 + aadlen;
+	r.payload_len = len;
+	r.digest_start = 16 + aadlen + len;
+	r.encrypt = encrypt;
+	e = swcr_eta_c(sa, &r);
+	if (e == 0) {
+		memcpy(data, buf + r.payload_start, (size_t)len);
+		if (encrypt)
+			memcpy(digest, buf + r.digest_start, (size_t)sa->mlen);
+	}
+	free(buf);
+	oref_sa_free(sa);
+	return e;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Multi-threaded batch driver (CPU baseline)                                */
+
+struct job {
+	oref_sa *const *sas;
+	uint8_t *arena;
+	const uint32_t *off4;
+	const uint16_t *len, *sa_idx;
+	const uint32_t *esn_hi;
+	uint8_t *status;
+	long lo, hi;
+	int encrypt;
+};
+
+static void *worker(void *arg)
+{
+	struct job *j = arg;
+
+	for (long i = j->lo; i < j->hi; i++) {
+		uint32_t e = j->esn_hi ? j->esn_hi[i] : 0;
+		int rc = esp_process(j->sas[j->sa_idx[i]], j->arena + (size_t)j->off4[i] * 4,
+		    j->len[i], e, j->encrypt);
+		if (j->status)
+			j->status[i] = (uint8_t)rc;
+	}
+	return NULL;
+}
+
+static double now_s(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static double run_batch(oref_sa *const *sas, uint8_t *arena, const uint32_t *off4,
+    const uint16_t *len, const uint16_t *sa_idx, const uint32_t *esn_hi,
+    uint8_t *status, long n, int nthreads, int encrypt)
+{
+	pthread_t th[256];
+	struct job jobs[256];
+	double t0, t1;
+
+	init_tables();
+	if (nthreads < 1)
+		nthreads = 1;
+	if (nthreads > 256)
+		nthreads = 256;
+	for (int t = 0; t < nthreads; t++) {
+		jobs[t] = (struct job){ sas, arena, off4, len, sa_idx, esn_hi, status,
+		    n * t / nthreads, n * (t + 1) / nthreads, encrypt };
+	}
+	t0 = now_s();
+	if (nthreads == 1) {
+		worker(&jobs[0]);
+	} else {
+		for (int t = 0; t < nthreads; t++)
+			pthread_create(&th[t], NULL, worker, &jobs[t]);
+		for (int t = 0; t < nthreads; t++)
+			pthread_join(th[t], NULL);
+	}
+	t1 = now_s();
+	return t1 - t0;
+}
+
+double oref_batch_decrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *off4,
+    const uint16_t *len, const uint16_t *sa_idx, const uint32_t *esn_hi,
+    uint8_t *status, long n, int nthreads)
+{
+	return run_batch(sas, arena, off4, len, sa_idx, esn_hi, status, n, nthreads, 0);
+}
+
+double oref_batch_encrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *off4,
+    const uint16_t *len, const uint16_t *sa_idx, const uint32_t *esn_hi,
+    long n, int nthreads)
+{
+	return run_batch(sas, arena, off4, len, sa_idx, esn_hi, NULL, n, nthreads, 1);
+}

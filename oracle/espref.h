@@ -1,0 +1,98 @@
+/*
+ * espref.h — CPU restatement of the F-Stack/FreeBSD ESP bulk-crypto path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle (and the "port"
+ * CPU baseline) for the MI355X engine in f-stack_amd/.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * The product path never links or calls anything in oracle/.
+ *
+ * What it restates (reference = /root/reference, F-Stack 1.25):
+ *   freebsd/crypto/rijndael/rijndael-alg-fst.c   AES T-table cipher + key schedules
+ *   freebsd/opencrypto/gfmult.c, gmac.c          GHASH (4-bit Shoup tables) / AES-GMAC
+ *   freebsd/opencrypto/xform_aes_icm.c           GCM counter mode (counter starts at 2)
+ *   freebsd/crypto/sha1.c, opencrypto/crypto.c   SHA-1 and HMAC ipad/opad precompute
+ *   freebsd/opencrypto/cryptosoft.c              swcr_gcm / swcr_eta / swcr_encdec /
+ *                                                swcr_authcompute request processing
+ *   freebsd/netipsec/xform_esp.c                 esp_input / esp_output request layout
+ *
+ * Pinning: primitives are checked against the reference's own
+ * rijndael-alg-fst.c / gfmult.c compiled from /root/reference (oracle/_ref),
+ * and whole-path results against DPDK's ESP / AEAD / CBC+HMAC-SHA1 known-answer
+ * vectors held in the reference tree (tests/golden/).
+ */
+#ifndef ESPREF_H
+#define ESPREF_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Session modes (values of crypto_session_params.csp_mode, cryptodev.h:360-365). */
+#define OREF_CSP_MODE_AEAD 4
+#define OREF_CSP_MODE_ETA  5
+/* csp_flags (cryptodev.h:369-371) */
+#define OREF_CSP_F_SEPARATE_AAD 0x0002
+#define OREF_CSP_F_ESN          0x0004
+/* algorithms (cryptodev.h:150-169) */
+#define OREF_CRYPTO_SHA1_HMAC      7
+#define OREF_CRYPTO_AES_CBC        11
+#define OREF_CRYPTO_AES_NIST_GCM_16 25
+
+typedef struct oref_sa oref_sa;
+
+/* --- primitives (for pinning against oracle/_ref and KATs) --- */
+int  oref_aes_setkey_enc(uint32_t rk[60], const uint8_t *key, int keybits);   /* returns Nr */
+int  oref_aes_setkey_dec(uint32_t rk[60], const uint8_t *key, int keybits);
+void oref_aes_encrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16]);
+void oref_aes_decrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16]);
+/* out = x * h in GF(2^128), GCM bit order (gfmult.c representation) */
+void oref_gf128_mul(const uint8_t h[16], const uint8_t x[16], uint8_t out[16]);
+void oref_sha1(const uint8_t *msg, size_t len, uint8_t out[20]);
+void oref_hmac_sha1(const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t out[20]);
+
+/* Generic AES-GCM AEAD (12-byte IV) as swcr_gcm computes it; in place.
+ * encrypt: writes tag[16].  decrypt: verifies tag[0..mlen) and returns
+ * 0 or EBADMSG (buffer untouched on EBADMSG). */
+int oref_gcm(const uint8_t *key, int klen, const uint8_t iv[12],
+             const uint8_t *aad, int aadlen, uint8_t *data, int len,
+             uint8_t *tag, int mlen, int encrypt);
+
+/* Generic AES-CBC + HMAC-SHA1 encrypt-then-MAC (swcr_eta) over
+ * [aad | data]; digest[20] written (encrypt) or its first mlen bytes checked. */
+int oref_eta(const uint8_t *ckey, int cklen, const uint8_t *akey, int aklen,
+             const uint8_t iv[16], const uint8_t *aad, int aadlen, uint8_t *data, int len,
+             uint8_t *digest, int mlen, int encrypt);
+
+/* --- sessions (swcr_newsession/swcr_setup_gcm/swcr_setup_cipher/auth) ---
+ * GCM: ckey is the SA key WITHOUT the 4-byte salt (esp_init strips it,
+ * xform_esp.c:169); salt is passed separately.
+ * ETA: AES-CBC cipher key + HMAC-SHA1 key, mlen 12 (AH_HMAC_HASHLEN). */
+oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
+                     const uint8_t salt[4], const uint8_t *akey, int aklen, int mlen);
+void oref_sa_free(oref_sa *sa);
+
+/* ESP record = [SPI 4][SN 4][IV ivlen][payload][ICV alen], i.e. the buffer
+ * esp_input sees at `skip` (xform_esp.c:260-463).  In place.
+ * Returns 0, EBADMSG (ICV mismatch, buffer untouched) or EINVAL (length). */
+int oref_esp_decrypt(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi);
+/* esp_output direction over an already padded record: encrypts payload and
+ * writes the ICV (xform_esp.c:673-961, cryptosoft.c:558-568,636). */
+int oref_esp_encrypt(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi);
+
+/* Batch decrypt with `nthreads` workers, each taking a contiguous slice
+ * (one private session per worker, like one F-Stack stack per lcore).
+ * rec i is at arena + off4[i]*4, length len[i], SA sas[sa_idx[i]].
+ * Returns wall seconds of the decrypt loop only. */
+double oref_batch_decrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *off4,
+                          const uint16_t *len, const uint16_t *sa_idx,
+                          const uint32_t *esn_hi, uint8_t *status, long n, int nthreads);
+double oref_batch_encrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *off4,
+                          const uint16_t *len, const uint16_t *sa_idx,
+                          const uint32_t *esn_hi, long n, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
