@@ -1,0 +1,395 @@
+// esp_gcm.hip — ESP AES-GCM-16 verify+decrypt / encrypt kernel for gfx950.
+//
+// Replaces swcr_gcm (freebsd/opencrypto/cryptosoft.c:465-645) as reached from
+// esp_input / esp_output (freebsd/netipsec/xform_esp.c:260-463, 673-961):
+//   AAD   = SPI||SN (8 B) or SPI||ESN_hi||SN (12 B, CSP_F_SEPARATE_AAD)
+//   nonce = salt(4) || explicit IV(8);  J0 = nonce||1;  CT block c uses nonce||c+2
+//   tag   = GHASH_H(AAD, CT, len) ^ E_K(J0), compared on mlen bytes; a mismatch
+//           sets EBADMSG and the record's plaintext is not released.
+//
+// Mapping (MI355X-first, not a translation of the 16-byte-at-a-time loop):
+//  * 8 lanes per ESP record, 8 records per wave, 16 waves per workgroup
+//    (a 128-record "chunk" of ONE session per workgroup iteration).
+//  * GHASH is reassociated so every lane runs a Horner chain with the SAME
+//    multiplier H^8 over blocks l, l+8, l+16, ... of its record (the block list
+//    is front-padded with zero blocks to a multiple of 8, which leaves the hash
+//    unchanged), then multiplies by H^(8-l) and the 8 partials are XOR-reduced
+//    across the lane group.  Multiplication by a fixed H^e uses 4-bit tables
+//    indexed per nibble POSITION (32 x 16 x 16 B per power, in LDS), so there
+//    is no shift/reduce step: X*H^e = XOR_j T_e[j][nib_j(X)].  Each 256-byte
+//    position table spans all 64 LDS banks once, so a ds_read_b128 lookup is
+//    bank-conflict-free whatever the nibble values.
+//  * AES-CTR uses one T-table of (Te0[x], Te1[x]) pairs replicated 32x in LDS
+//    (entry x at x*256, lane slot (lane&31)*8): ds_read_b64 with every lane of a
+//    32-lane group on its own bank pair -> conflict-free; the LDS address is a
+//    single v_perm_b32 of (state byte, lane slot).  Te2/Te3 are folded through
+//    one ror16 per column: t = Te0[a]^Te1[b]^ror16(Te0[c]^Te1[d]^ror16(rk)).
+//  * The lane that owns GHASH block i also computes AES(nonce||i+1): block 0
+//    (the AAD block) gets J0, CT block c = i-1 gets counter c+2, so the CTR
+//    work is perfectly aligned with the hash work and plaintext is stored from
+//    the same registers that fed GHASH.
+//  * Records and descriptors are read with 16-byte loads, 128 contiguous bytes
+//    per lane group per step.  HBM traffic per record = record + descriptor +
+//    plaintext + status byte.
+#include <hip/hip_runtime.h>
+
+#include "espgpu_internal.h"
+
+namespace espgpu {
+
+namespace {
+
+constexpr uint32_t LDS_TP = 0;          // 256 entries x 32 lane slots x 8 B
+constexpr uint32_t LDS_GT = 65536;      // 8 powers x 32 positions x 16 x 16 B
+constexpr uint32_t LDS_RK = 131072;     // 64 words round keys (kernel form)
+constexpr uint32_t LDS_BYTES = LDS_RK + 64 * 4;
+constexpr int WG = 1024;
+constexpr int S = 8;                    // lanes per record
+
+struct __attribute__((aligned(4))) U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t ror16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return perm(x, x, 0x00010203u); }
+
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+  U4 v = *reinterpret_cast<const U4 *>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
+  U4 u{v.x, v.y, v.z, v.w};
+  *reinterpret_cast<U4 *>(p) = u;
+}
+
+// Keep the first `rem` bytes (1..16) of a 16-byte block, zero the rest.
+__device__ __forceinline__ uint4 mask_block(uint4 v, int rem) {
+  if (rem >= 16) return v;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int b = rem - 4 * k;
+    uint32_t m = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+    w[k] &= m;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Store the first `rem` bytes of v (ESP payloads are 4-byte multiples; the
+// byte tail keeps generic GCM lengths exact).
+__device__ __forceinline__ void st_partial(uint8_t *p, uint4 v, int rem) {
+  if (rem >= 16) {
+    st16(p, v);
+    return;
+  }
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int b = rem - 4 * k;
+    if (b >= 4) {
+      *reinterpret_cast<uint32_t *>(p + 4 * k) = w[k];
+    } else if (b > 0) {
+      for (int t = 0; t < b; ++t) p[4 * k + t] = (uint8_t)(w[k] >> (8 * t));
+    }
+  }
+}
+
+// ---- AES (rijndaelEncrypt, rijndael-alg-fst.c:863-1042) on the pair table ----
+
+// LDS byte address of the pair for byte k of w: byte0 = lane slot, byte1 = w.byte k.
+__device__ __forceinline__ uint32_t tpa(uint32_t w, uint32_t slot, int k) {
+  return perm(w, slot, 0x0c0c0000u | ((4u + (uint32_t)k) << 8));
+}
+
+template <int NR>
+__device__ __forceinline__ uint4 aes_enc(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                         const uint8_t *lds, uint32_t slot) {
+  // s* are big-endian state words already XORed with rk[0..3].
+  const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LDS_RK);
+#pragma unroll
+  for (int r = 1; r < NR; ++r) {
+    uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * r);
+    uint2 a0 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 3));
+    uint2 b0 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 2));
+    uint2 c0 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 1));
+    uint2 d0 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 0));
+    uint2 a1 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 3));
+    uint2 b1 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 2));
+    uint2 c1 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 1));
+    uint2 d1 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 0));
+    uint2 a2 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 3));
+    uint2 b2 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 2));
+    uint2 c2 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 1));
+    uint2 d2 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 0));
+    uint2 a3 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 3));
+    uint2 b3 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 2));
+    uint2 c3 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 1));
+    uint2 d3 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 0));
+    s0 = xor3(a0.x, b0.y, ror16(xor3(c0.x, d0.y, k.x)));
+    s1 = xor3(a1.x, b1.y, ror16(xor3(c1.x, d1.y, k.y)));
+    s2 = xor3(a2.x, b2.y, ror16(xor3(c2.x, d2.y, k.z)));
+    s3 = xor3(a3.x, b3.y, ror16(xor3(c3.x, d3.y, k.w)));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
+  // words directly; the last round key is stored byte-swapped.
+  uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * NR);
+  const uint32_t *t32 = reinterpret_cast<const uint32_t *>(lds);
+  uint32_t a, b, c, d, o[4];
+  uint32_t ss[4] = {s0, s1, s2, s3};
+  uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+  for (int col = 0; col < 4; ++col) {
+    a = t32[tpa(ss[col], slot, 3) >> 2];
+    b = t32[tpa(ss[(col + 1) & 3], slot, 2) >> 2];
+    c = t32[tpa(ss[(col + 2) & 3], slot, 1) >> 2];
+    d = t32[tpa(ss[(col + 3) & 3], slot, 0) >> 2];
+    o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// ---- GHASH multiply by a fixed power (gf128_mul, gfmult.c:219-229) ----------
+// pb = LDS byte address of the power's 8 KiB table (low byte 0, < 2^24).
+__device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds) {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t hi = w[k] & 0xF0F0F0F0u;           // high nibble * 16, per byte
+    const uint32_t lo = (w[k] << 4) & 0xF0F0F0F0u;    // low nibble * 16, per byte
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t sel = 0x0c060500u | (uint32_t)q;
+      const uint32_t alo = perm(pb, lo, sel);
+      const uint32_t ahi = perm(pb, hi, sel);
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + alo + (8 * k + 2 * q) * 256);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + ahi + (8 * k + 2 * q + 1) * 256);
+      r0 = xor3(r0, e.x, f.x);
+      r1 = xor3(r1, e.y, f.y);
+      r2 = xor3(r2, e.z, f.z);
+      r3 = xor3(r3, e.w, f.w);
+    }
+    // bound the lookahead to 8 lookups (32 VGPRs) so the hoisted loads do not spill
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return make_uint4(r0, r1, r2, r3);
+}
+
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
+  return make_uint4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
+}
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
+  return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+
+// ---- one 8-record group per wave -----------------------------------------------
+// MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
+// MODE 1: encrypt in place + ICV
+// MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
+template <int MODE, int NR>
+__device__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
+                         uint32_t sa, uint32_t sa_flags, uint32_t mlen) {
+  const int lane = threadIdx.x & 63;
+  const int l = lane & (S - 1);
+  const uint32_t slot = (uint32_t)(lane & 31) * 8;
+  const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LDS_RK);
+
+  // -- descriptor and record header ------------------------------------------
+  int valid = 0, ct_len = 0, nct = 0, N = 0, M = 0, pad = 0;
+  size_t base = 0;
+  uint32_t len = 0;
+  uint4 aadblk = make_uint4(0, 0, 0, 0), lenblk = make_uint4(0, 0, 0, 0);
+  uint32_t s0c = 0, s1c = 0, s2c = 0;
+  if (have) {
+    const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+    base = (size_t)dv.x * 4;
+    len = dv.y & 0xffffu;
+    const uint32_t dsa = dv.y >> 16;
+    ct_len = (int)len - 32;                        // 8 hdr + 8 IV + 16 ICV
+    valid = (dsa == sa) && ct_len > 0 && (len & 3) == 0;   // xform_esp.c:279-324
+    if (valid) {
+      const uint2 hdr = *reinterpret_cast<const uint2 *>(p.arena + base);       // SPI, SN
+      const uint2 iv = *reinterpret_cast<const uint2 *>(p.arena + base + 8);    // explicit IV
+      const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
+      const uint32_t aad_len = sep ? 12 : 8;
+      aadblk = sep ? make_uint4(hdr.x, bswap32(dv.z), hdr.y, 0) : make_uint4(hdr.x, hdr.y, 0, 0);
+      lenblk = make_uint4(0, bswap32(aad_len * 8), 0, bswap32((uint32_t)ct_len * 8));
+      nct = (ct_len + 15) >> 4;
+      N = nct + 2;
+      M = (N + S - 1) / S;
+      pad = S * M - N;
+      s0c = bswap32(dv.w) ^ rk[0];                 // salt
+      s1c = bswap32(iv.x) ^ rk[1];
+      s2c = bswap32(iv.y) ^ rk[2];
+    }
+  }
+  int Mw = M;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Mw = max(Mw, __shfl_xor(Mw, o));
+  if (Mw == 0) {
+    if (have && l == 0 && !valid) p.status[di] = ESPGPU_EINVAL;
+    return;
+  }
+  const uint32_t rk3 = rk[3];
+  uint8_t *rec = p.arena + base;
+  uint8_t *orec = (MODE == 0 ? p.out : p.arena) + base;
+
+  uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
+  for (int m = 0; m < Mw; ++m) {
+    const int i = S * m + l - pad;
+    if (m > 0) Y = gf_mul(Y, LDS_GT + 7 * 8192, lds);          // * H^8
+    uint4 ks = make_uint4(0, 0, 0, 0);
+    if (MODE != 2 || i == 0)
+      ks = aes_enc<NR>(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, lds, slot);
+    uint4 B = make_uint4(0, 0, 0, 0);
+    if (valid && i >= 1 && i <= nct) {
+      const int c = i - 1;
+      const int rem = ct_len - 16 * c;
+      const uint4 C = ld16(rec + 16 + 16 * c);
+      if (MODE == 1) {
+        const uint4 o = xor4(C, ks);
+        st_partial(orec + 16 + 16 * c, o, rem);
+        B = mask_block(o, rem);
+      } else {
+        B = mask_block(C, rem);
+        if (MODE == 0) st_partial(orec + 16 + 16 * c, xor4(C, ks), rem);
+      }
+    } else if (i == 0) {
+      B = aadblk;
+      EJ0 = ks;
+    } else if (i == N - 1) {
+      B = lenblk;
+    }
+    Y = xor4(Y, B);
+  }
+  // X = sum_l Y_l * H^(8-l)  (power index 7-l)
+  uint4 Z = gf_mul(Y, LDS_GT + (uint32_t)(7 - l) * 8192, lds);
+  Z = xor4(Z, shfl_xor4(Z, 1));
+  Z = xor4(Z, shfl_xor4(Z, 2));
+  Z = xor4(Z, shfl_xor4(Z, 4));
+  const uint4 ej0 = shfl4(EJ0, (lane & ~(S - 1)) | pad);
+  const uint4 T = xor4(Z, ej0);
+
+  int ok = 1;
+  if (valid) {
+    const size_t icv = len - 16;
+    if (MODE == 1) {
+      if (l == 0) st_partial(rec + icv, T, (int)mlen);
+    } else {
+      const uint4 tag = ld16(rec + icv);
+      const uint4 d = mask_block(xor4(T, tag), (int)mlen);
+      ok = ((d.x | d.y | d.z | d.w) == 0);
+    }
+  }
+  if (MODE == 2) {
+    // pass 2: CTR decrypt in place, only for authenticated records
+    const int run = valid && ok;
+    int Mr = run ? M : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
+    for (int m = 0; m < Mr; ++m) {
+      const int i = S * m + l - pad;
+      const uint4 ks = aes_enc<NR>(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, lds, slot);
+      if (run && i >= 1 && i <= nct) {
+        const int c = i - 1;
+        const uint4 C = ld16(rec + 16 + 16 * c);
+        st_partial(rec + 16 + 16 * c, xor4(C, ks), ct_len - 16 * c);
+      }
+    }
+  }
+  if (have && l == 0)
+    p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(WG, 1) void gcm_kernel(GcmParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const int tid = threadIdx.x;
+
+  // Pair table, replicated into 32 lane slots per entry.
+  for (int idx = tid; idx < 256 * 32; idx += WG) {
+    const int x = idx >> 5, r = idx & 31;
+    *reinterpret_cast<uint2 *>(lds + LDS_TP + x * 256 + r * 8) = p.tpair[x];
+  }
+
+  const bool implicit = (p.chunks == nullptr);
+  const uint32_t nch = implicit ? (p.n + kChunkRecs - 1) / kChunkRecs : *p.nchunks;
+  const uint32_t c0 = (uint32_t)(((uint64_t)blockIdx.x * nch) / gridDim.x);
+  const uint32_t c1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * nch) / gridDim.x);
+  uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
+  const int wave = tid >> 6;
+
+  for (uint32_t c = c0; c < c1; ++c) {
+    uint32_t sa, start, count;
+    if (implicit) {
+      start = c * kChunkRecs;
+      count = min((uint32_t)kChunkRecs, p.n - start);
+      sa = p.desc[start].sa;
+    } else {
+      const Chunk ch = p.chunks[c];
+      sa = ch.sa;
+      start = ch.start;
+      count = ch.count;
+    }
+    sa = __builtin_amdgcn_readfirstlane(sa);
+    if (sa != cur_sa) {
+      __syncthreads();
+      if (sa < p.nsas) {
+        const DevSA *s = p.sas + sa;
+        nr = s->nr;
+        flags = s->flags;
+        mlen = s->mlen;
+        mode = s->mode;
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
+#pragma unroll 4
+        for (int q = tid; q < (int)(kGhTableBytes / 16); q += WG) dst[q] = src[q];
+        if (tid < 64) reinterpret_cast<uint32_t *>(lds + LDS_RK)[tid] = s->rk[tid];
+      } else {
+        mode = 0;
+      }
+      cur_sa = sa;
+      __syncthreads();
+    }
+    const uint32_t rl = (uint32_t)wave * S + ((tid & 63) >> 3);
+    const bool have = rl < count;
+    const uint32_t pos = start + (have ? rl : 0);
+    const uint32_t di = p.order ? p.order[pos] : pos;
+    if (mode != ESPGPU_CSP_MODE_AEAD) {
+      if (have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
+      continue;
+    }
+    if (nr == 10)
+      do_group<MODE, 10>(p, lds, di, have, sa, flags, mlen);
+    else if (nr == 12)
+      do_group<MODE, 12>(p, lds, di, have, sa, flags, mlen);
+    else
+      do_group<MODE, 14>(p, lds, di, have, sa, flags, mlen);
+  }
+}
+
+}  // namespace
+
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (grid <= 0) grid = 256;
+  if (encrypt)
+    hipLaunchKernelGGL(gcm_kernel<1>, dim3(grid), dim3(WG), 0, st, p);
+  else if (two_pass)
+    hipLaunchKernelGGL(gcm_kernel<2>, dim3(grid), dim3(WG), 0, st, p);
+  else
+    hipLaunchKernelGGL(gcm_kernel<0>, dim3(grid), dim3(WG), 0, st, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace espgpu

@@ -1,0 +1,589 @@
+// espgpu.cpp — host runtime behind include/espgpu.h: the opencrypto-driver
+// shaped C ABI (sessions, process/flush/poll with pinned staging and async
+// copies on a HIP stream) and the device-resident batch entry points.
+//
+// Reference interfaces mirrored (F-Stack 1.25 tree):
+//   probesession  freebsd/opencrypto/cryptosoft.c:1244-1303 (swcr_probesession)
+//                 + check_csp, freebsd/opencrypto/crypto.c:746-870
+//   newsession    cryptosoft.c:1309-1409, swcr_setup_gcm :1087, _cipher :976, _auth :1003
+//   freesession   cryptosoft.c:1412
+//   process       cryptosoft.c:1429-1441 (swcr_process) -> swcr_gcm :465 / swcr_eta :874
+//   completion    crypto_done, crypto.c:1802
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "espgpu.h"
+#include "espgpu_internal.h"
+#include "host_crypto.h"
+
+#ifndef ERESTART
+#define ERESTART 85   /* FreeBSD's value is -1 in-kernel; Linux has 85. */
+#endif
+
+using namespace espgpu;
+
+namespace {
+
+struct Session {
+  bool used = false;
+  int mode = 0, flags = 0, mlen = 0, klen = 0;
+};
+
+struct Pending {
+  void *opaque;
+  int etype_pre;              // -1: take the device status; else a host-side errno
+  uint32_t rec;               // descriptor index in the batch
+  uint32_t stage_off;         // byte offset of the staged record
+  uint32_t stage_len;
+  // where the result bytes go back: [buf_off, buf_off+n) of the request buffer
+  // receives staged bytes [stage_from, stage_from+n); up to 2 spans
+  struct Span { uint32_t buf_off, stage_from, n; } span[2];
+  int nspan;
+  std::vector<espgpu_seg> segs;
+};
+
+enum { SLOT_FREE = 0, SLOT_FILLING = 1, SLOT_INFLIGHT = 2 };
+
+struct Slot {
+  int state = SLOT_FREE;
+  int op = -1;                // 0 decrypt, 1 encrypt
+  uint8_t *h_arena = nullptr, *d_arena = nullptr, *d_out = nullptr;
+  espgpu_desc *h_desc = nullptr, *d_desc = nullptr;
+  uint8_t *h_status = nullptr, *d_status = nullptr;
+  uint32_t nrec = 0, bytes = 0;
+  std::vector<Pending> reqs;
+  hipEvent_t done = nullptr;
+};
+
+}  // namespace
+
+struct espgpu_ctx {
+  int device = 0;
+  espgpu_config cfg{};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevSA *d_sas = nullptr;
+  uint8_t *d_gtab = nullptr;
+  uint2 *d_tpair = nullptr, *d_dpair = nullptr;
+  uint8_t *d_isbox = nullptr;
+  std::vector<Session> sessions;
+  std::vector<DevSA> h_sas;
+  int n_eta = 0;
+  // planner workspace
+  uint32_t plan_cap = 0;
+  uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
+  Chunk *d_chunks = nullptr;
+  uint32_t max_chunks = 0;
+  // staging
+  std::vector<Slot> slots;
+  int cur = 0;
+  std::vector<espgpu_completion> ready;   // host-side completions (EINVAL etc.)
+  espgpu_stats stats{};
+  float last_ms = 0.f;
+  std::string err;
+};
+
+namespace {
+
+int fail(espgpu_ctx *c, int code, const char *fmt, ...) {
+  if (c) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                          \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) return fail(ctx, EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+uint32_t be32(const uint8_t *p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
+uint32_t ror16(uint32_t v) { return (v >> 16) | (v << 16); }
+
+int ensure_plan(espgpu_ctx *c, uint32_t n) {
+  const uint32_t nsas = (uint32_t)c->sessions.size();
+  const uint32_t need_chunks = n / kChunkRecs + 4 * nsas + 8;
+  if (n <= c->plan_cap && need_chunks <= c->max_chunks) return 0;
+  hipFree(c->d_work);
+  hipFree(c->d_order);
+  hipFree(c->d_chunks);
+  hipFree(c->d_nchunks);
+  c->plan_cap = std::max(n, 1024u);
+  c->max_chunks = c->plan_cap / kChunkRecs + 4 * nsas + 8;
+  HIPCHK(c, hipMalloc(&c->d_work, plan_workspace_words(nsas) * 4));
+  HIPCHK(c, hipMalloc(&c->d_order, (size_t)c->plan_cap * 4));
+  HIPCHK(c, hipMalloc(&c->d_chunks, (size_t)c->max_chunks * sizeof(Chunk)));
+  HIPCHK(c, hipMalloc(&c->d_nchunks, 16));
+  return 0;
+}
+
+// Copy `n` bytes at logical offset `off` of a segmented buffer.
+bool seg_copy_out(const std::vector<espgpu_seg> &segs, uint32_t off, uint32_t n, uint8_t *dst) {
+  for (const auto &s : segs) {
+    if (off >= s.len) { off -= s.len; continue; }
+    uint32_t k = std::min(n, s.len - off);
+    memcpy(dst, (const uint8_t *)s.base + off, k);
+    dst += k; n -= k; off = 0;
+    if (!n) return true;
+  }
+  return n == 0;
+}
+bool seg_copy_in(const std::vector<espgpu_seg> &segs, uint32_t off, uint32_t n, const uint8_t *src) {
+  for (const auto &s : segs) {
+    if (off >= s.len) { off -= s.len; continue; }
+    uint32_t k = std::min(n, s.len - off);
+    memcpy((uint8_t *)s.base + off, src, k);
+    src += k; n -= k; off = 0;
+    if (!n) return true;
+  }
+  return n == 0;
+}
+
+int alloc_slot(espgpu_ctx *c, Slot &s) {
+  const size_t bytes = c->cfg.batch_bytes + 64, recs = c->cfg.batch_records;
+  HIPCHK(c, hipHostMalloc((void **)&s.h_arena, bytes, hipHostMallocDefault));
+  HIPCHK(c, hipHostMalloc((void **)&s.h_desc, recs * sizeof(espgpu_desc), hipHostMallocDefault));
+  HIPCHK(c, hipHostMalloc((void **)&s.h_status, recs, hipHostMallocDefault));
+  HIPCHK(c, hipMalloc(&s.d_arena, bytes));
+  HIPCHK(c, hipMalloc(&s.d_out, bytes));
+  HIPCHK(c, hipMalloc(&s.d_desc, recs * sizeof(espgpu_desc)));
+  HIPCHK(c, hipMalloc(&s.d_status, recs));
+  HIPCHK(c, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  return 0;
+}
+
+void free_slot(Slot &s) {
+  hipHostFree(s.h_arena); hipHostFree(s.h_desc); hipHostFree(s.h_status);
+  hipFree(s.d_arena); hipFree(s.d_out); hipFree(s.d_desc); hipFree(s.d_status);
+  if (s.done) hipEventDestroy(s.done);
+}
+
+// Launch the crypto kernels for one batch of device-resident records.
+int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
+              uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st) {
+  if (n == 0) return 0;
+  const uint32_t nsas = (uint32_t)c->sessions.size();
+  GcmParams p{};
+  p.arena = d_arena;
+  p.out = encrypt ? d_arena : (d_out ? d_out : d_arena);
+  p.desc = d_desc;
+  p.n = n;
+  p.sas = c->d_sas;
+  p.gtab = c->d_gtab;
+  p.tpair = c->d_tpair;
+  p.status = d_status;
+  p.nsas = nsas;
+  if (!(flags & ESPGPU_BATCH_GROUPED)) {
+    int e = ensure_plan(c, n);
+    if (e) return e;
+    if (launch_plan(d_desc, n, c->d_sas, nsas, c->d_work, c->d_order, c->d_chunks, c->d_nchunks,
+                    c->max_chunks, st))
+      return fail(c, ENOTSUP, "planner: too many sessions for device grouping (%u); pre-group and pass ESPGPU_BATCH_GROUPED", nsas);
+    p.order = c->d_order;
+    p.chunks = c->d_chunks;
+    p.nchunks = c->d_nchunks;
+  }
+  const int two_pass = (!encrypt && p.out == d_arena);
+  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st)) return fail(c, EIO, "GCM kernel launch failed");
+  if (c->n_eta > 0) {
+    EtaParams q{};
+    q.arena = d_arena;
+    q.out = p.out;
+    q.desc = d_desc;
+    q.n = n;
+    q.sas = c->d_sas;
+    q.tpair = c->d_tpair;
+    q.dpair = c->d_dpair;
+    q.isbox = c->d_isbox;
+    q.status = d_status;
+    q.nsas = nsas;
+    if (launch_eta(q, encrypt, (int)c->cfg.grid, st)) return fail(c, EIO, "ETA kernel launch failed");
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int espgpu_abi_version(void) { return ESPGPU_ABI_VERSION; }
+
+const char *espgpu_last_error(espgpu_ctx *c) { return c ? c->err.c_str() : "no context"; }
+
+int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
+  if (!out) return EINVAL;
+  *out = nullptr;
+  espgpu_ctx *c = new espgpu_ctx();
+  espgpu_config cfg{};
+  if (cfg_in) cfg = *cfg_in;
+  if (!cfg.max_sessions) cfg.max_sessions = 1024;
+  if (!cfg.batch_records) cfg.batch_records = 65536;
+  if (!cfg.batch_bytes) cfg.batch_bytes = 64u << 20;
+  if (!cfg.nbatches) cfg.nbatches = 2;
+  c->cfg = cfg;
+  c->device = cfg.device;
+  int rc = 0;
+  do {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg.device) {
+      rc = fail(c, ENODEV, "no HIP device %d (found %d)", cfg.device, ndev);
+      break;
+    }
+    if (hipSetDevice(cfg.device) != hipSuccess) { rc = fail(c, ENODEV, "hipSetDevice failed"); break; }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = fail(c, EIO, "stream"); break; }
+    hipEventCreate(&c->ev0);
+    hipEventCreate(&c->ev1);
+    if (hipMalloc(&c->d_sas, (size_t)cfg.max_sessions * sizeof(DevSA)) != hipSuccess ||
+        hipMalloc(&c->d_gtab, (size_t)cfg.max_sessions * kGhTableBytes) != hipSuccess ||
+        hipMalloc(&c->d_tpair, 256 * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&c->d_dpair, 256 * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&c->d_isbox, 256) != hipSuccess) {
+      rc = fail(c, ENOMEM, "device SA table allocation failed");
+      break;
+    }
+    hipMemset(c->d_sas, 0, (size_t)cfg.max_sessions * sizeof(DevSA));
+    const hc::Tables &t = hc::tables();
+    uint2 tp[256], dp[256];
+    for (int x = 0; x < 256; ++x) {
+      tp[x] = make_uint2(t.te0[x], (t.te0[x] >> 8) | (t.te0[x] << 24));
+      dp[x] = make_uint2(t.td0[x], (t.td0[x] >> 8) | (t.td0[x] << 24));
+    }
+    hipMemcpy(c->d_tpair, tp, sizeof tp, hipMemcpyHostToDevice);
+    hipMemcpy(c->d_dpair, dp, sizeof dp, hipMemcpyHostToDevice);
+    hipMemcpy(c->d_isbox, t.isbox, 256, hipMemcpyHostToDevice);
+    c->slots.resize(cfg.nbatches);
+    for (auto &s : c->slots)
+      if ((rc = alloc_slot(c, s))) break;
+  } while (0);
+  if (rc) {
+    fprintf(stderr, "espgpu_init: %s\n", c->err.c_str());
+    espgpu_fini(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
+void espgpu_fini(espgpu_ctx *c) {
+  if (!c) return;
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (auto &s : c->slots) free_slot(s);
+  hipFree(c->d_sas); hipFree(c->d_gtab); hipFree(c->d_tpair); hipFree(c->d_dpair); hipFree(c->d_isbox);
+  hipFree(c->d_work); hipFree(c->d_order); hipFree(c->d_chunks); hipFree(c->d_nchunks);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+// swcr_probesession + check_csp restricted to the ESP ciphers this engine serves.
+int espgpu_probesession(const espgpu_session_params *csp) {
+  if (!csp) return EINVAL;
+  const int supported_flags = ESPGPU_CSP_F_SEPARATE_AAD | ESPGPU_CSP_F_ESN;
+  if (csp->csp_flags & ~supported_flags) return EINVAL;
+  if (csp->csp_ivlen < 0 || csp->csp_cipher_klen < 0 || csp->csp_auth_klen < 0 || csp->csp_auth_mlen < 0)
+    return EINVAL;
+  const int k = csp->csp_cipher_klen;
+  const bool aes_klen = (k == 16 || k == 24 || k == 32);
+  switch (csp->csp_mode) {
+    case ESPGPU_CSP_MODE_AEAD:
+      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_NIST_GCM_16 || !aes_klen) return EINVAL;
+      if (csp->csp_ivlen != 12) return EINVAL;                 // cryptosoft.c:1093
+      if (csp->csp_auth_alg != 0 || csp->csp_auth_klen != 0) return EINVAL;
+      if (csp->csp_auth_mlen > 16) return EINVAL;
+      if (csp->csp_flags & ESPGPU_CSP_F_ESN) return EINVAL;    // ESN for GCM = SEPARATE_AAD
+      return ESPGPU_PROBE_HARDWARE;
+    case ESPGPU_CSP_MODE_ETA:
+      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC || !aes_klen) return EINVAL;
+      if (csp->csp_ivlen != 16) return EINVAL;
+      if (csp->csp_auth_alg != ESPGPU_CRYPTO_SHA1_HMAC || csp->csp_auth_klen <= 0) return EINVAL;
+      if (csp->csp_auth_mlen > 20) return EINVAL;
+      if (csp->csp_flags & ESPGPU_CSP_F_SEPARATE_AAD) return EINVAL;
+      return ESPGPU_PROBE_HARDWARE;
+    default:
+      return EINVAL;
+  }
+}
+
+int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *sid_out) {
+  if (!c || !csp || !sid_out) return EINVAL;
+  int pr = espgpu_probesession(csp);
+  if (pr >= 0) return fail(c, EINVAL, "session parameters not supported");
+  if (!csp->csp_cipher_key) return fail(c, EINVAL, "per-request keys are not supported; session key required");
+  int slot = -1;
+  for (size_t i = 0; i < c->sessions.size(); ++i)
+    if (!c->sessions[i].used) { slot = (int)i; break; }
+  if (slot < 0) {
+    if (c->sessions.size() >= c->cfg.max_sessions) return fail(c, ENOMEM, "SA table full (%u)", c->cfg.max_sessions);
+    slot = (int)c->sessions.size();
+    c->sessions.emplace_back();
+    c->h_sas.emplace_back();
+  }
+  DevSA sa;
+  memset(&sa, 0, sizeof sa);
+  const uint8_t *key = (const uint8_t *)csp->csp_cipher_key;
+  uint32_t rk[60];
+  const int nr = hc::aes_expand_enc(key, csp->csp_cipher_klen, rk);
+  sa.nr = (uint32_t)nr;
+  sa.mode = (uint32_t)csp->csp_mode;
+  sa.flags = (uint32_t)csp->csp_flags;
+  if (csp->csp_mode == ESPGPU_CSP_MODE_AEAD) {
+    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : 16;
+    // kernel form: raw first round, ror16 middle rounds, byte-swapped last round
+    for (int i = 0; i < 4; ++i) sa.rk[i] = rk[i];
+    for (int i = 4; i < 4 * nr; ++i) sa.rk[i] = ror16(rk[i]);
+    for (int i = 0; i < 4; ++i) sa.rk[4 * nr + i] = bswap(rk[4 * nr + i]);
+    uint8_t zero[16] = {0}, h[16];
+    hc::aes_encrypt_block(rk, nr, zero, h);       // H = E_K(0^128), gmac.c:56-60
+    std::vector<uint8_t> tabs(kGhTableBytes);
+    hc::ghash_tables(h, tabs.data());
+    HIPCHK(c, hipMemcpy(c->d_gtab + (size_t)slot * kGhTableBytes, tabs.data(), kGhTableBytes, hipMemcpyHostToDevice));
+  } else {
+    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : 20;
+    for (int i = 0; i < 4 * (nr + 1); ++i) sa.rk[i] = rk[i];
+    uint32_t dk[60];
+    hc::aes_expand_dec(key, csp->csp_cipher_klen, dk);
+    for (int i = 0; i < 4 * (nr + 1); ++i) sa.dk[i] = dk[i];
+    hc::hmac_sha1_pad_state((const uint8_t *)csp->csp_auth_key, csp->csp_auth_klen, 0x36, sa.ipad);
+    hc::hmac_sha1_pad_state((const uint8_t *)csp->csp_auth_key, csp->csp_auth_klen, 0x5c, sa.opad);
+    c->n_eta++;
+  }
+  HIPCHK(c, hipMemcpy(c->d_sas + slot, &sa, sizeof sa, hipMemcpyHostToDevice));
+  Session &s = c->sessions[slot];
+  s.used = true;
+  s.mode = csp->csp_mode;
+  s.flags = csp->csp_flags;
+  s.mlen = (int)sa.mlen;
+  s.klen = csp->csp_cipher_klen;
+  c->h_sas[slot] = sa;
+  *sid_out = slot;
+  return 0;
+}
+
+void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
+  if (!c || sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return;
+  // Records already flushed keep their results; wait so the slot is not reused under them.
+  hipStreamSynchronize(c->stream);
+  if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
+  c->sessions[sid] = Session();
+  DevSA z;
+  memset(&z, 0, sizeof z);
+  hipMemcpy(c->d_sas + sid, &z, sizeof z, hipMemcpyHostToDevice);
+}
+
+// Validate that a request has the shape esp_input / esp_output build
+// (xform_esp.c:364-461, 820-900) and stage it as an ESP wire record.
+int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
+  (void)hint;
+  if (!c || !r) return EINVAL;
+  Slot *s = &c->slots[c->cur];
+  if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ERESTART; }
+  const int op = (r->crp_op & ESPGPU_CRYPTO_OP_ENCRYPT) ? 1 : 0;
+  if (s->state == SLOT_FILLING && s->op != op) {
+    int e = espgpu_flush(c);
+    if (e) return e;
+    s = &c->slots[c->cur];
+    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ERESTART; }
+  }
+  auto reject = [&](int etype) {
+    c->ready.push_back(espgpu_completion{r->opaque, etype});
+    if (etype == EINVAL) c->stats.einval++;
+    return 0;
+  };
+  const int sid = r->session;
+  if (sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return reject(EINVAL);
+  const Session &ses = c->sessions[sid];
+  size_t total = 0;
+  for (int i = 0; i < r->nsegs; ++i) total += r->segs[i].len;
+  const bool gcm = ses.mode == ESPGPU_CSP_MODE_AEAD;
+  const int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen, alen = gcm ? 16 : ses.mlen;
+  const int plen = r->crp_payload_length;
+  int aad_start = r->crp_aad_start;
+  // ESP shape checks
+  if (plen <= 0 || r->crp_payload_start < 0 || (size_t)(r->crp_digest_start + alen) > total) return reject(EINVAL);
+  uint8_t hdr[8];
+  uint32_t esn_hi = 0, salt = 0;
+  if (gcm) {
+    if (!(r->crp_flags & ESPGPU_CRYPTO_F_IV_SEPARATE)) return reject(EINVAL);   // cryptosoft.c:496
+    if (r->crp_aad) {
+      if (!(ses.flags & ESPGPU_CSP_F_SEPARATE_AAD) || r->crp_aad_length != 12) return reject(EINVAL);
+      const uint8_t *a = (const uint8_t *)r->crp_aad;
+      memcpy(hdr, a, 4);
+      memcpy(hdr + 4, a + 8, 4);
+      esn_hi = be32(a + 4);
+      aad_start = r->crp_payload_start - hlen;   // header bytes in the buffer (unused by the cipher)
+    } else {
+      if (r->crp_aad_length != 8 || (ses.flags & ESPGPU_CSP_F_SEPARATE_AAD)) return reject(EINVAL);
+      if (r->crp_payload_start != aad_start + hlen) return reject(EINVAL);
+      std::vector<espgpu_seg> sv(r->segs, r->segs + r->nsegs);
+      if (!seg_copy_out(sv, (uint32_t)aad_start, 8, hdr)) return reject(EINVAL);
+    }
+    salt = le32(r->crp_iv);
+  } else {
+    if (r->crp_aad || r->crp_aad_length != hlen || r->crp_iv_start != aad_start + 8 ||
+        r->crp_payload_start != aad_start + hlen || (plen & 15))
+      return reject(EINVAL);
+    if (ses.flags & ESPGPU_CSP_F_ESN) esn_hi = be32(r->crp_esn);
+  }
+  if (r->crp_digest_start != r->crp_payload_start + plen) return reject(EINVAL);
+  const uint32_t rlen = (uint32_t)(hlen + plen + alen);
+  if (rlen > 65535 || (rlen & 3)) return reject(EINVAL);
+  if (s->nrec >= c->cfg.batch_records || s->bytes + rlen + 16 > c->cfg.batch_bytes) {
+    int e = espgpu_flush(c);
+    if (e) return e;
+    s = &c->slots[c->cur];
+    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ERESTART; }
+  }
+  if (s->state == SLOT_FREE) {
+    s->state = SLOT_FILLING;
+    s->op = op;
+    s->nrec = 0;
+    s->bytes = 0;
+    s->reqs.clear();
+  }
+  Pending pd;
+  pd.opaque = r->opaque;
+  pd.etype_pre = -1;
+  pd.rec = s->nrec;
+  pd.stage_off = s->bytes;
+  pd.stage_len = rlen;
+  pd.segs.assign(r->segs, r->segs + r->nsegs);
+  uint8_t *dst = s->h_arena + s->bytes;
+  bool ok;
+  if (gcm) {
+    memcpy(dst, hdr, 8);
+    memcpy(dst + 8, r->crp_iv + 4, 8);
+    ok = seg_copy_out(pd.segs, (uint32_t)r->crp_payload_start, (uint32_t)(plen + alen), dst + hlen);
+  } else {
+    ok = seg_copy_out(pd.segs, (uint32_t)aad_start, rlen, dst);
+  }
+  if (!ok) return reject(EINVAL);
+  // results: payload (+ digest when encrypting) go back to the request buffer
+  pd.nspan = 1;
+  pd.span[0] = {(uint32_t)r->crp_payload_start, (uint32_t)hlen, (uint32_t)plen};
+  if (op == 1) {
+    pd.nspan = 2;
+    pd.span[1] = {(uint32_t)r->crp_digest_start, (uint32_t)(hlen + plen), (uint32_t)ses.mlen};
+  }
+  espgpu_desc &d = s->h_desc[s->nrec];
+  d.off4 = s->bytes / 4;
+  d.len = (uint16_t)rlen;
+  d.sa = (uint16_t)sid;
+  d.esn_hi = esn_hi;
+  d.salt = salt;
+  s->bytes += (rlen + 15) & ~15u;
+  s->nrec++;
+  s->reqs.push_back(std::move(pd));
+  return 0;
+}
+
+int espgpu_flush(espgpu_ctx *c) {
+  if (!c) return EINVAL;
+  Slot &s = c->slots[c->cur];
+  if (s.state != SLOT_FILLING || s.nrec == 0) return 0;
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(s.d_arena, s.h_arena, s.bytes + 16, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(s.d_desc, s.h_desc, s.nrec * sizeof(espgpu_desc), hipMemcpyHostToDevice, st));
+  hipEventRecord(c->ev0, st);
+  int e = run_batch(c, s.d_arena, s.d_desc, s.nrec, s.d_status, s.op ? nullptr : s.d_out, 0, s.op, st);
+  if (e) return e;
+  hipEventRecord(c->ev1, st);
+  HIPCHK(c, hipMemcpyAsync(s.h_arena, s.op ? s.d_arena : s.d_out, s.bytes, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(s.h_status, s.d_status, s.nrec, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipEventRecord(s.done, st));
+  s.state = SLOT_INFLIGHT;
+  c->stats.batches++;
+  c->cur = (c->cur + 1) % (int)c->slots.size();
+  return 0;
+}
+
+static int complete_slot(espgpu_ctx *c, Slot &s) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) {
+    c->last_ms = ms;
+    c->stats.kernel_ns += (uint64_t)(ms * 1e6);
+  }
+  for (auto &pd : s.reqs) {
+    int et = pd.etype_pre >= 0 ? pd.etype_pre : (int)s.h_status[pd.rec];
+    if (et == 0) {
+      const uint8_t *src = s.h_arena + pd.stage_off;
+      for (int k = 0; k < pd.nspan; ++k)
+        seg_copy_in(pd.segs, pd.span[k].buf_off, pd.span[k].n, src + pd.span[k].stage_from);
+      c->stats.bytes += pd.span[0].n;
+    } else if (et == EBADMSG) {
+      c->stats.auth_fail++;
+    } else {
+      c->stats.einval++;
+    }
+    c->stats.records++;
+    c->ready.push_back(espgpu_completion{pd.opaque, et});
+  }
+  s.reqs.clear();
+  s.nrec = 0;
+  s.bytes = 0;
+  s.state = SLOT_FREE;
+  return 0;
+}
+
+int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
+  if (!c) return -EINVAL;
+  // completions of flushed batches, oldest first
+  for (size_t k = 0; k < c->slots.size(); ++k) {
+    Slot &s = c->slots[(c->cur + k) % c->slots.size()];
+    if (s.state != SLOT_INFLIGHT) continue;
+    if (hipEventQuery(s.done) != hipSuccess) continue;
+    complete_slot(c, s);
+  }
+  int n = std::min<int>(max, (int)c->ready.size());
+  for (int i = 0; i < n; ++i) out[i] = c->ready[i];
+  c->ready.erase(c->ready.begin(), c->ready.begin() + n);
+  return n;
+}
+
+int espgpu_drain(espgpu_ctx *c) {
+  if (!c) return EINVAL;
+  int e = espgpu_flush(c);
+  if (e) return e;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (auto &s : c->slots)
+    if (s.state == SLOT_INFLIGHT) complete_slot(c, s);
+  return 0;
+}
+
+int espgpu_get_stats(espgpu_ctx *c, espgpu_stats *st) {
+  if (!c || !st) return EINVAL;
+  *st = c->stats;
+  return 0;
+}
+
+int espgpu_decrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
+                         uint8_t *d_status, uint8_t *d_out, uint32_t flags, void *stream) {
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return EINVAL;
+  return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
+                   reinterpret_cast<hipStream_t>(stream));
+}
+
+int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
+                         uint8_t *d_status, uint32_t flags, void *stream) {
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return EINVAL;
+  return run_batch(c, d_arena, d_desc, n, d_status, nullptr, flags, 1, reinterpret_cast<hipStream_t>(stream));
+}
+
+float espgpu_last_kernel_ms(espgpu_ctx *c) { return c ? c->last_ms : 0.f; }
+
+}  // extern "C"

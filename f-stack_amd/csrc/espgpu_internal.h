@@ -1,0 +1,84 @@
+// espgpu_internal.h — device-side data layouts shared by the host runtime
+// (espgpu.cpp) and the HIP kernels (esp_gcm.hip, esp_cbc.hip, plan.hip).
+#pragma once
+#include <stdint.h>
+
+#include "espgpu.h"
+
+namespace espgpu {
+
+// ---- per-SA device record (one per session slot), 1 KiB ----------------------
+// GCM: rk[] is the AES encryption schedule in "kernel form" for the pair-table
+//   round (see esp_gcm.hip):  rk[0..3] raw, rk[4r..4r+3] = ror16(rk) for the
+//   middle rounds, rk[4nr..] byte-swapped (the last round emits little-endian
+//   words).  The GHASH tables live in a separate 64 KiB-per-slot array.
+// ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
+//   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
+//   = SHA-1 chaining state after one block of key^0x36 / key^0x5c
+//   (hmac_init_pad, crypto.c:413-441).
+struct DevSA {
+  uint32_t rk[64];
+  uint32_t dk[64];
+  uint32_t nr;
+  uint32_t mode;    // ESPGPU_CSP_MODE_AEAD / _ETA, 0 = free slot
+  uint32_t flags;   // csp_flags
+  uint32_t mlen;    // ICV bytes compared / written
+  uint32_t ipad[5];
+  uint32_t opad[5];
+  uint32_t pad_[256 - 128 - 4 - 10];
+};
+static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
+
+// GHASH multiplication tables for one SA: powers H^1..H^8, 32 nibble
+// positions, 16 nibble values, 16-byte products in memory byte order.
+constexpr int kGhPowers = 8;
+constexpr uint32_t kGhTableBytes = kGhPowers * 32 * 16 * 16;   // 65536
+
+// A chunk: up to kChunkRecs records of ONE session, processed by one
+// workgroup iteration of the GCM kernel.  rec positions index `order`
+// (or the descriptor array directly when order == nullptr).
+constexpr int kChunkRecs = 128;
+struct Chunk {
+  uint32_t sa;
+  uint32_t start;
+  uint32_t count;
+  uint32_t cls;     // size class (planner); informational
+};
+
+struct GcmParams {
+  uint8_t *arena;                 // records (read; written in place for encrypt)
+  uint8_t *out;                   // decrypt output (may == arena)
+  const espgpu_desc *desc;
+  const uint32_t *order;          // planner permutation or nullptr
+  const Chunk *chunks;            // explicit chunk list, or nullptr (implicit)
+  const uint32_t *nchunks;        // device count of explicit chunks
+  uint32_t n;                     // number of descriptors (implicit mode)
+  const DevSA *sas;
+  const uint8_t *gtab;            // [slot][65536]
+  const uint2 *tpair;             // 256 x (Te0[x], Te1[x])
+  uint8_t *status;
+  uint32_t nsas;
+};
+
+struct EtaParams {
+  uint8_t *arena;
+  uint8_t *out;
+  const espgpu_desc *desc;
+  uint32_t n;
+  const DevSA *sas;
+  const uint2 *tpair;             // encryption pair table
+  const uint2 *dpair;             // decryption pair table (Td0, Td1)
+  const uint8_t *isbox;           // inverse S-box (256 B)
+  uint8_t *status;
+  uint32_t nsas;
+};
+
+// Launchers (defined in the .hip files, called by espgpu.cpp).
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream);
+int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream);
+int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
+                uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
+                uint32_t max_chunks, void *stream);
+size_t plan_workspace_words(uint32_t nsas);
+
+}  // namespace espgpu

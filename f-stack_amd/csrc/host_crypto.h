@@ -1,0 +1,37 @@
+// host_crypto.h — session-setup arithmetic run on the host at newsession time
+// (the work swcr_setup_gcm / swcr_setup_cipher / swcr_setup_auth do in
+// freebsd/opencrypto/cryptosoft.c:976-1128): AES key schedules, H = E_K(0),
+// GHASH power tables, HMAC-SHA1 ipad/opad chaining states.  Nothing here runs
+// per packet; the per-packet work is all in the HIP kernels.
+#pragma once
+#include <stdint.h>
+
+namespace espgpu {
+namespace hc {
+
+struct Tables {
+  uint8_t sbox[256], isbox[256];
+  uint32_t te0[256], td0[256];   // big-endian T-table words
+};
+const Tables &tables();
+
+// FIPS-197 key expansion; returns Nr (10/12/14) or 0 on a bad length.
+int aes_expand_enc(const uint8_t *key, int klen_bytes, uint32_t rk[60]);
+// Equivalent-inverse-cipher schedule (rijndaelKeySetupDec layout).
+int aes_expand_dec(const uint8_t *key, int klen_bytes, uint32_t dk[60]);
+void aes_encrypt_block(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16]);
+
+// GF(2^128) product in GCM bit order (SP 800-38D Algorithm 1).
+void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
+
+// 64 KiB GHASH table set for the GCM kernel: powers H^1..H^8, per nibble
+// position j (byte j>>1, low nibble if j even), per nibble value.
+void ghash_tables(const uint8_t h[16], uint8_t *out65536);
+
+// SHA-1 compression of one 64-byte block into state h[5].
+void sha1_compress(uint32_t h[5], const uint8_t block[64]);
+// HMAC pad state: h = SHA1-compress(IV, (key or SHA1(key)) ^ padval).
+void hmac_sha1_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t h[5]);
+
+}  // namespace hc
+}  // namespace espgpu

@@ -1,0 +1,157 @@
+// plan.hip — device-side batch planner: groups ESP records by (size class,
+// session) so that each 128-record chunk of the GCM kernel has ONE session
+// (its GHASH power tables and round keys are staged once in LDS) and records
+// of similar length share a wave.  Three small kernels, no host round trip:
+//   plan_count   per-workgroup LDS histogram of keys, flushed with one global
+//                atomic per non-empty key per workgroup
+//   plan_scan    one workgroup: exclusive scan of key counts -> record offsets
+//                and chunk offsets; writes the chunk list and its length
+//   plan_scatter per-workgroup LDS ranks + one global range reservation per
+//                non-empty key -> order[] (a permutation of descriptor ids)
+// Keys: [0, 4*nsas) = GCM records (class-major), 4*nsas = records of ETA
+// sessions (not chunked: the ETA kernel walks descriptors directly),
+// 4*nsas+1 = records with no valid session (chunked with sa = ~0 so the GCM
+// kernel marks them EINVAL).  Cost: two passes over the 16-byte descriptors.
+#include <hip/hip_runtime.h>
+
+#include "espgpu_internal.h"
+
+namespace espgpu {
+
+namespace {
+
+constexpr int PWG = 1024;
+constexpr int PER_THREAD = 4;
+constexpr int TILE = PWG * PER_THREAD;
+constexpr uint32_t kMaxLdsKeys = 16384;   // 64 KiB per LDS array
+
+__device__ __forceinline__ uint32_t size_class(uint32_t len) {
+  // GHASH blocks N = ceil((len-32)/16) + 2; steps per lane M = ceil(N/8)
+  const int ct = (int)len - 32;
+  const int n = (ct > 0 ? (ct + 15) >> 4 : 0) + 2;
+  const int m = (n + 7) >> 3;
+  return m <= 1 ? 0u : (m <= 4 ? 1u : (m <= 16 ? 2u : 3u));
+}
+
+__device__ __forceinline__ uint32_t key_of(const espgpu_desc &d, const DevSA *sas, uint32_t nsas) {
+  const uint32_t sa = d.sa;
+  if (sa >= nsas) return 4 * nsas + 1;
+  const uint32_t mode = sas[sa].mode;
+  if (mode == ESPGPU_CSP_MODE_ETA) return 4 * nsas;
+  if (mode != ESPGPU_CSP_MODE_AEAD) return 4 * nsas + 1;
+  return size_class(d.len) * nsas + sa;
+}
+
+__global__ __launch_bounds__(PWG) void plan_count(const espgpu_desc *desc, uint32_t n,
+                                                  const DevSA *sas, uint32_t nsas,
+                                                  uint32_t *gcnt) {
+  __shared__ uint32_t hist[kMaxLdsKeys];
+  const uint32_t nkeys = 4 * nsas + 2;
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) hist[k] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * TILE;
+#pragma unroll
+  for (int j = 0; j < PER_THREAD; ++j) {
+    const uint32_t i = base + j * PWG + threadIdx.x;
+    if (i < n) atomicAdd(&hist[key_of(desc[i], sas, nsas)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG)
+    if (hist[k]) atomicAdd(&gcnt[k], hist[k]);
+}
+
+// Single workgroup.  gcnt[nkeys] -> gcur[nkeys] (record cursor), chunks.
+__global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t nsas,
+                                                 uint32_t *gcur, Chunk *chunks,
+                                                 uint32_t *nchunks, uint32_t max_chunks) {
+  __shared__ uint32_t s_rec[PWG], s_chk[PWG];
+  const uint32_t nkeys = 4 * nsas + 2;
+  const uint32_t per = (nkeys + PWG - 1) / PWG;
+  const uint32_t k0 = threadIdx.x * per, k1 = min(nkeys, k0 + per);
+  auto is_chunked = [&](uint32_t k) { return k != 4 * nsas; };
+  uint32_t r = 0, c = 0;
+  for (uint32_t k = k0; k < k1; ++k) {
+    r += gcnt[k];
+    if (is_chunked(k)) c += (gcnt[k] + kChunkRecs - 1) / kChunkRecs;
+  }
+  s_rec[threadIdx.x] = r;
+  s_chk[threadIdx.x] = c;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partials
+  for (int o = 1; o < PWG; o <<= 1) {
+    uint32_t a = threadIdx.x >= (unsigned)o ? s_rec[threadIdx.x - o] : 0;
+    uint32_t b = threadIdx.x >= (unsigned)o ? s_chk[threadIdx.x - o] : 0;
+    __syncthreads();
+    s_rec[threadIdx.x] += a;
+    s_chk[threadIdx.x] += b;
+    __syncthreads();
+  }
+  uint32_t roff = s_rec[threadIdx.x] - r, coff = s_chk[threadIdx.x] - c;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t cnt = gcnt[k];
+    gcur[k] = roff;
+    if (is_chunked(k)) {
+      const uint32_t sa = (k == 4 * nsas + 1) ? 0xffffffffu : k % nsas;
+      const uint32_t cls = (k == 4 * nsas + 1) ? 0u : k / nsas;
+      for (uint32_t j = 0; j * kChunkRecs < cnt; ++j, ++coff) {
+        if (coff < max_chunks)
+          chunks[coff] = Chunk{sa, roff + j * kChunkRecs, min((uint32_t)kChunkRecs, cnt - j * kChunkRecs), cls};
+      }
+    }
+    roff += cnt;
+  }
+  if (threadIdx.x == PWG - 1) *nchunks = min(s_chk[PWG - 1], max_chunks);
+}
+
+__global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uint32_t n,
+                                                    const DevSA *sas, uint32_t nsas,
+                                                    uint32_t *gcur, uint32_t *order) {
+  __shared__ uint32_t hist[kMaxLdsKeys], lbase[kMaxLdsKeys];
+  const uint32_t nkeys = 4 * nsas + 2;
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) hist[k] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * TILE;
+  uint32_t key[PER_THREAD], rank[PER_THREAD];
+#pragma unroll
+  for (int j = 0; j < PER_THREAD; ++j) {
+    const uint32_t i = base + j * PWG + threadIdx.x;
+    key[j] = 0xffffffffu;
+    if (i < n) {
+      key[j] = key_of(desc[i], sas, nsas);
+      rank[j] = atomicAdd(&hist[key[j]], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG)
+    if (hist[k]) lbase[k] = atomicAdd(&gcur[k], hist[k]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER_THREAD; ++j) {
+    const uint32_t i = base + j * PWG + threadIdx.x;
+    if (i < n) order[lbase[key[j]] + rank[j]] = i;
+  }
+}
+
+}  // namespace
+
+// gcnt[nkeys] + gcur[nkeys]
+size_t plan_workspace_words(uint32_t nsas) { return 2 * (size_t)(4 * nsas + 2); }
+
+int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
+                uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
+                uint32_t max_chunks, void *stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t nkeys = 4 * nsas + 2;
+  if (nkeys > kMaxLdsKeys) return -1;     // caller must pre-group (ESPGPU_BATCH_GROUPED)
+  uint32_t *gcnt = d_work, *gcur = d_work + nkeys;
+  if (hipMemsetAsync(gcnt, 0, nkeys * sizeof(uint32_t), st) != hipSuccess) return -1;
+  const uint32_t grid = (n + TILE - 1) / TILE;
+  if (grid) hipLaunchKernelGGL(plan_count, dim3(grid), dim3(PWG), 0, st, d_desc, n, sas, nsas, gcnt);
+  hipLaunchKernelGGL(plan_scan, dim3(1), dim3(PWG), 0, st, gcnt, nsas, gcur, d_chunks, d_nchunks,
+                     max_chunks);
+  if (grid) hipLaunchKernelGGL(plan_scatter, dim3(grid), dim3(PWG), 0, st, d_desc, n, sas, nsas, gcur,
+                               d_order);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace espgpu

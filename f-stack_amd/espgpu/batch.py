@@ -1,0 +1,48 @@
+"""Device-resident batch path (espgpu_decrypt_batch / espgpu_encrypt_batch).
+
+Records live in a torch.uint8 CUDA tensor (the arena, HBM), one 16-byte
+espgpu_desc per record in a second tensor.  torch is plumbing here: device
+memory and streams.  All crypto runs in libespgpu.so's HIP kernels.
+"""
+import numpy as np
+
+from . import _lib as L
+
+DESC_DTYPE = np.dtype([("off4", "<u4"), ("len", "<u2"), ("sa", "<u2"),
+                       ("esn_hi", "<u4"), ("salt", "<u4")])
+assert DESC_DTYPE.itemsize == 16
+
+
+def descs_to_tensor(descs, device):
+    """numpy structured DESC_DTYPE array -> uint8 CUDA tensor (n*16 bytes)."""
+    import torch
+    raw = np.ascontiguousarray(descs).view(np.uint8)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def decrypt_batch(driver, arena, desc, n, status, out=None, grouped=False, stream=None):
+    """Verify+decrypt n records.  out=None -> in place (verify-first two-pass)."""
+    for t in (arena, desc, status) + ((out,) if out is not None else ()):
+        assert t.is_cuda and t.is_contiguous()
+    rc = driver.lib.espgpu_decrypt_batch(
+        driver.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(),
+        out.data_ptr() if out is not None else None,
+        L.BATCH_GROUPED if grouped else 0, _stream_ptr(stream))
+    if rc:
+        raise RuntimeError("espgpu_decrypt_batch: %s" % driver.last_error())
+
+
+def encrypt_batch(driver, arena, desc, n, status, grouped=False, stream=None):
+    for t in (arena, desc, status):
+        assert t.is_cuda and t.is_contiguous()
+    rc = driver.lib.espgpu_encrypt_batch(
+        driver.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(),
+        L.BATCH_GROUPED if grouped else 0, _stream_ptr(stream))
+    if rc:
+        raise RuntimeError("espgpu_encrypt_batch: %s" % driver.last_error())

@@ -1,0 +1,142 @@
+"""ESP request builders, the caller side of the hot path (unchanged semantics).
+
+  esp_csp()           esp_init           freebsd/netipsec/xform_esp.c:143-244
+  esp_input_crp()     esp_input          xform_esp.c:260-463
+  esp_output_crp()    esp_output         xform_esp.c:673-961 (padding :710-716, :810-843)
+  esp_trailer_ok()    esp_input_cb tail  xform_esp.c:597-636
+Records are IPv4 packets with the ESP header at `skip` (tunnel mode: skip = IP
+header length), in a bytearray (or an mbuf-like list of bytearrays).
+"""
+import struct
+
+from . import _lib as L
+from .opencrypto import crypto_session_params
+
+GCM, CBC_SHA1 = "aes-gcm-16", "aes-cbc-hmac-sha1-96"
+IPPROTO_NONE = 59
+
+
+class SecAssoc:
+    """What key_setsaval leaves in struct secasvar for the two ESP transforms."""
+
+    def __init__(self, spi, alg, key, auth_key=b"", esn=False):
+        self.spi = spi
+        self.alg = alg
+        self.key = bytes(key)          # GCM: cipher key || 4-byte salt (RFC 4106 8.1)
+        self.auth_key = bytes(auth_key)
+        self.esn = esn
+
+    @property
+    def ivlen(self):
+        return 8 if self.alg == GCM else 16
+
+    @property
+    def hlen(self):
+        return 8 + self.ivlen           # struct newesp + IV
+
+    @property
+    def alen(self):
+        return 16 if self.alg == GCM else 12   # xform_ah_authsize: GMAC 16, SHA1-HMAC 12
+
+    @property
+    def blocksize(self):
+        return 1 if self.alg == GCM else 16   # enc_xform blocksize (ESP pads to 4 anyway)
+
+    @property
+    def salt(self):
+        return self.key[-4:] if self.alg == GCM else b"\0\0\0\0"
+
+    def csp(self):
+        if self.alg == GCM:
+            return crypto_session_params(
+                csp_mode=L.CSP_MODE_AEAD,
+                csp_flags=L.CSP_F_SEPARATE_AAD if self.esn else 0,
+                csp_ivlen=12, csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16,
+                csp_cipher_klen=len(self.key) - 4, csp_cipher_key=self.key[:-4])
+        return crypto_session_params(
+            csp_mode=L.CSP_MODE_ETA, csp_flags=L.CSP_F_ESN if self.esn else 0,
+            csp_ivlen=16, csp_cipher_alg=L.CRYPTO_AES_CBC, csp_cipher_klen=len(self.key),
+            csp_cipher_key=self.key, csp_auth_alg=L.CRYPTO_SHA1_HMAC,
+            csp_auth_klen=len(self.auth_key), csp_auth_key=self.auth_key, csp_auth_mlen=12)
+
+
+def _flat(buf):
+    return bytes(buf) if not isinstance(buf, list) else b"".join(bytes(b) for b in buf)
+
+
+def esp_input_crp(fw, ses, sa, pkt, skip, esn_hi=0):
+    """Build the decrypt+verify cryptop exactly as esp_input does."""
+    total = len(_flat(pkt))
+    crp = fw.crypto_getreq(ses)
+    crp.crp_op = L.CRYPTO_OP_VERIFY_DIGEST | L.CRYPTO_OP_DECRYPT
+    crp.crp_aad_length = 8 if sa.alg == GCM else sa.hlen                      # :366-369
+    seqh = struct.pack(">I", esn_hi)
+    data = _flat(pkt)
+    if sa.alg == GCM and sa.esn:                                              # :372-397
+        crp.crp_aad = data[skip:skip + 4] + seqh + data[skip + 4:skip + 8]
+        crp.crp_aad_length = 12
+    else:
+        crp.crp_aad_start = skip
+    if sa.alg != GCM and sa.esn:
+        crp.crp_esn = seqh                                                    # :400-402
+    crp.crp_digest_start = total - sa.alen                                    # :404
+    crp.crp_flags = L.CRYPTO_F_CBIFSYNC
+    crp.crp_buf = pkt
+    crp.crp_payload_start = skip + sa.hlen                                    # :424-425
+    crp.crp_payload_length = total - (skip + sa.hlen + sa.alen)
+    if sa.alg == GCM:                                                         # :430-455
+        crp.crp_iv = bytearray(sa.salt + data[skip + sa.hlen - sa.ivlen:skip + sa.hlen] + b"\0" * 4)
+        crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
+    else:
+        crp.crp_iv_start = skip + sa.hlen - sa.ivlen
+    return crp
+
+
+def esp_output_crp(fw, ses, sa, pkt, skip, esn_hi=0):
+    """The encrypt cryptop esp_output builds over an already padded packet."""
+    total = len(_flat(pkt))
+    data = _flat(pkt)
+    crp = fw.crypto_getreq(ses)
+    crp.crp_op = L.CRYPTO_OP_ENCRYPT | L.CRYPTO_OP_COMPUTE_DIGEST
+    crp.crp_flags = L.CRYPTO_F_CBIFSYNC
+    crp.crp_buf = pkt
+    crp.crp_payload_start = skip + sa.hlen
+    crp.crp_payload_length = total - (skip + sa.hlen + sa.alen)
+    crp.crp_digest_start = total - sa.alen
+    seqh = struct.pack(">I", esn_hi)
+    if sa.alg == GCM:
+        if sa.esn:
+            crp.crp_aad = data[skip:skip + 4] + seqh + data[skip + 4:skip + 8]
+            crp.crp_aad_length = 12
+        else:
+            crp.crp_aad_start = skip
+            crp.crp_aad_length = 8
+        crp.crp_iv = bytearray(sa.salt + data[skip + 8:skip + 16] + b"\0" * 4)
+        crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
+    else:
+        crp.crp_aad_start = skip
+        crp.crp_aad_length = sa.hlen
+        crp.crp_iv_start = skip + 8
+        if sa.esn:
+            crp.crp_esn = seqh
+    return crp
+
+
+def esp_pad(inner, blocksize=4, next_header=4):
+    """Self-describing padding 1,2,3,... + pad length + next header (xform_esp.c:810-843)."""
+    rlen = len(inner)
+    padding = ((blocksize - ((rlen + 2) % blocksize)) % blocksize) + 2
+    pad = bytes(range(1, padding - 1)) + bytes([padding - 2, next_header])
+    return bytes(inner) + pad
+
+
+def esp_trailer_ok(plain_payload):
+    """The checks esp_input_cb makes on the last three plaintext bytes
+    (xform_esp.c:597-630, default SADB_X_EXT_PSEQ padding)."""
+    p = bytes(plain_payload)
+    last = p[-3:]
+    if last[1] + 2 > len(p):
+        return False
+    if last[1] != last[0] and last[1] != 0:
+        return False
+    return last[2] != IPPROTO_NONE

@@ -1,0 +1,186 @@
+/*
+ * espgpu.h — C ABI of the MI355X-native ESP bulk-crypto engine (libespgpu.so).
+ *
+ * Drop-in boundary: this library plays the part of an opencrypto *driver*
+ * (freebsd/opencrypto/cryptodev_if.m) beneath the unchanged opencrypto
+ * framework, i.e. it replaces the software driver "cryptosoft"
+ * (freebsd/opencrypto/cryptosoft.c) for the ESP ciphers F-Stack's IPsec uses:
+ *   AES-GCM-16 (CSP_MODE_AEAD)                  -> swcr_gcm      cryptosoft.c:465-645
+ *   AES-CBC + HMAC-SHA1-96 (CSP_MODE_ETA)       -> swcr_eta      cryptosoft.c:874-888
+ * Every entry point is plain C: integers, pointers, sizes.  No exceptions,
+ * no C++ or torch types cross it.  Errors are errno values, as in opencrypto.
+ * One espgpu_ctx per lcore thread (thread-compatible, not thread-safe), the
+ * way F-Stack runs one FreeBSD stack per lcore (lib/ff_dpdk_if.c:2235).
+ *
+ * Two ways in:
+ *  (1) the opencrypto driver path (host buffers): probesession / newsession /
+ *      freesession / process / flush / poll  — what a kernel-domain driver shim
+ *      in F-Stack binds;
+ *  (2) the device-resident batch path: records already in HBM, a 16-byte
+ *      descriptor per record — what bench.py times and what a GPU-direct RX
+ *      path would call.
+ */
+#ifndef ESPGPU_H
+#define ESPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ESPGPU_ABI_VERSION 1
+
+/* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
+#define ESPGPU_CSP_MODE_AEAD        4        /* cryptodev.h:364 */
+#define ESPGPU_CSP_MODE_ETA         5        /* cryptodev.h:365 */
+#define ESPGPU_CSP_F_SEPARATE_AAD   0x0002   /* cryptodev.h:370 */
+#define ESPGPU_CSP_F_ESN            0x0004   /* cryptodev.h:371 */
+#define ESPGPU_CRYPTO_SHA1_HMAC     7        /* cryptodev.h:150 */
+#define ESPGPU_CRYPTO_AES_CBC       11       /* cryptodev.h:155 */
+#define ESPGPU_CRYPTO_AES_NIST_GCM_16 25     /* cryptodev.h:169 */
+#define ESPGPU_CRYPTO_OP_DECRYPT    0x0      /* cryptodev.h:598 */
+#define ESPGPU_CRYPTO_OP_ENCRYPT    0x1
+#define ESPGPU_CRYPTO_OP_VERIFY_DIGEST 0x2
+#define ESPGPU_CRYPTO_F_IV_SEPARATE 0x0200   /* cryptodev.h:470 */
+#define ESPGPU_CRYPTO_HINT_MORE     0x1      /* cryptodev.h:612 */
+#define ESPGPU_PROBE_HARDWARE       (-100)   /* CRYPTODEV_PROBE_HARDWARE, cryptodev.h:345 */
+
+/* Status byte values written per record by the device (errno values). */
+#define ESPGPU_OK       0
+#define ESPGPU_EINVAL   22
+#define ESPGPU_EBADMSG  74
+
+/* Mirror of struct crypto_session_params (cryptodev.h:357-384). */
+struct espgpu_session_params {
+	int         csp_mode;
+	int         csp_flags;
+	int         csp_ivlen;
+	int         csp_cipher_alg;
+	int         csp_cipher_klen;
+	const void *csp_cipher_key;
+	int         csp_auth_alg;
+	int         csp_auth_klen;
+	const void *csp_auth_key;
+	int         csp_auth_mlen;
+};
+
+/* One buffer segment (an mbuf in the chain, or the whole contiguous buffer). */
+struct espgpu_seg {
+	void    *base;
+	uint32_t len;
+};
+
+/*
+ * Mirror of the struct cryptop fields a driver consumes (cryptodev.h:427-504).
+ * The buffer is crp_buf (CRYPTO_BUF_CONTIG = 1 segment, CRYPTO_BUF_MBUF = the
+ * chain as segments), processed in place.  `opaque` comes back in the
+ * completion (a kernel-domain shim passes the cryptop pointer itself).
+ */
+struct espgpu_req {
+	int32_t                  session;
+	int                      crp_op;
+	int                      crp_flags;
+	const struct espgpu_seg *segs;
+	int                      nsegs;
+	const void              *crp_aad;          /* separate AAD or NULL */
+	int                      crp_aad_start;
+	int                      crp_aad_length;
+	uint8_t                  crp_esn[4];
+	int                      crp_iv_start;
+	int                      crp_payload_start;
+	int                      crp_payload_length;
+	int                      crp_digest_start;
+	uint8_t                  crp_iv[16];
+	void                    *opaque;
+};
+
+struct espgpu_completion {
+	void *opaque;
+	int   etype;            /* crp_etype: 0, EBADMSG, EINVAL, ENOMEM, EAGAIN */
+};
+
+/* Device-resident descriptor: one per ESP record (16 bytes). */
+struct espgpu_desc {
+	uint32_t off4;          /* record start in the arena, in 4-byte units       */
+	uint16_t len;           /* ESP record length: SPI|SN|IV|payload|ICV          */
+	uint16_t sa;            /* session slot (espgpu_newsession's id)             */
+	uint32_t esn_hi;        /* high 32 bits of the ESN (SAs with CSP_F_ESN/SEP)  */
+	uint32_t salt;          /* GCM nonce salt = crp_iv[0..3] as stored in memory */
+};
+
+struct espgpu_config {
+	int      device;          /* HIP device ordinal                               */
+	uint32_t max_sessions;    /* SA table capacity (default 1024)                 */
+	uint32_t batch_records;   /* records per host batch (default 65536)           */
+	uint32_t batch_bytes;     /* staging bytes per host batch (default 64 MiB)    */
+	uint32_t nbatches;        /* staging slots in flight (default 2)              */
+	uint32_t grid;            /* workgroups for the crypto kernels (0 = auto)     */
+};
+
+struct espgpu_stats {
+	uint64_t records, bytes, auth_fail, einval;
+	uint64_t batches, kernel_ns;   /* kernel_ns: device time measured with events */
+	uint64_t erestart;
+};
+
+typedef struct espgpu_ctx espgpu_ctx;
+
+/* ---- lifecycle (a kernel-domain shim calls crypto_get_driverid(...,
+ *      CRYPTOCAP_F_HARDWARE|CRYPTOCAP_F_SYNC), crypto.c:989, around these) ---- */
+int  espgpu_abi_version(void);
+int  espgpu_init(const struct espgpu_config *cfg, espgpu_ctx **out);
+void espgpu_fini(espgpu_ctx *ctx);
+const char *espgpu_last_error(espgpu_ctx *ctx);
+
+/* ---- opencrypto driver methods (cryptodev_if.m) ---- */
+/* CRYPTODEV_PROBESESSION (cryptodev_if.m:72-75): ESPGPU_PROBE_HARDWARE or EINVAL.
+ * Host-only; no device needed. */
+int  espgpu_probesession(const struct espgpu_session_params *csp);
+/* CRYPTODEV_NEWSESSION (cryptodev_if.m:93-97): expands keys (AES schedule,
+ * GHASH power tables, HMAC ipad/opad states) into the device SA table. */
+int  espgpu_newsession(espgpu_ctx *ctx, const struct espgpu_session_params *csp,
+                       int32_t *session_out);
+/* CRYPTODEV_FREESESSION (cryptodev_if.m:113-116) */
+void espgpu_freesession(espgpu_ctx *ctx, int32_t session);
+/* CRYPTODEV_PROCESS (cryptodev_if.m:143-147): never blocks.  Stages the
+ * request; returns 0, or ERESTART when the staging batch is full (the framework
+ * then sets cc_qblocked and requeues, crypto.c:1451-1459).  Malformed requests
+ * complete with crp_etype = EINVAL via poll(), as crypto_done would. */
+int  espgpu_process(espgpu_ctx *ctx, const struct espgpu_req *req, int hint);
+/* Launch everything staged so far (H2D, kernels, D2H on the ctx stream).
+ * F-Stack's main_loop calls this once per RX burst (lib/ff_dpdk_if.c:2363). */
+int  espgpu_flush(espgpu_ctx *ctx);
+/* Complete finished requests: copies results back into the caller's segments
+ * (only for etype 0: EBADMSG leaves the buffer unchanged) and returns up to
+ * `max` completions; the shim calls crypto_done() for each. */
+int  espgpu_poll(espgpu_ctx *ctx, struct espgpu_completion *out, int max);
+/* Block until everything flushed has completed (teardown / tests). */
+int  espgpu_drain(espgpu_ctx *ctx);
+int  espgpu_get_stats(espgpu_ctx *ctx, struct espgpu_stats *st);
+
+/* ---- device-resident batch path ----
+ * d_arena: device buffer holding the records (padded by >= 16 bytes at its
+ * end); d_desc[n]; d_status[n] receives one errno byte per record.
+ * decrypt: plaintext goes to d_out at the same offsets (d_out may equal
+ * d_arena: then a verify-first two-pass kernel keeps EBADMSG records intact).
+ * encrypt: payload encrypted in place, ICV written.
+ * `flags`: ESPGPU_BATCH_GROUPED if d_desc is already grouped by session with
+ * at most one session per run of 128 records (skips the device planner).
+ * `stream` is a hipStream_t (NULL = default stream).  Asynchronous. */
+#define ESPGPU_BATCH_GROUPED 0x1
+int  espgpu_decrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
+                          uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t flags,
+                          void *stream);
+int  espgpu_encrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
+                          uint32_t n, uint8_t *d_status, uint32_t flags, void *stream);
+
+/* Device time of the last batch's crypto kernel (ms, from HIP events on the
+ * batch stream), for the roofline accounting in bench.py. */
+float espgpu_last_kernel_ms(espgpu_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESPGPU_H */

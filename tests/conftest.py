@@ -1,0 +1,30 @@
+"""pytest setup: import paths, the `gpu` marker, and on-demand native builds.
+
+The native artefacts (.so) are git-ignored; they are rebuilt here if missing
+so a fresh checkout runs.  `make` is incremental, so this is a no-op when the
+libraries are up to date.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "f-stack_amd"), os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _make(args):
+    try:
+        subprocess.run(["make", "-s"] + args, cwd=ROOT, check=True, timeout=900,
+                       stdout=subprocess.DEVNULL)
+    except Exception as e:  # surfaced by the tests that need the artefact
+        print("conftest: make %s failed: %s" % (" ".join(args), e), file=sys.stderr)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    _make(["-C", "oracle", "liboracle.so"])
+    if os.path.isdir("/root/reference/freebsd"):
+        _make(["-C", "oracle", "ref"])
+    _make(["-C", "f-stack_amd", "-j8"])

@@ -1,0 +1,86 @@
+"""Shared test fixtures: synthetic ESP records built and checked with the oracle."""
+import json
+import os
+
+import numpy as np
+
+import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+DESC = np.dtype([("off4", "<u4"), ("len", "<u2"), ("sa", "<u2"), ("esn_hi", "<u4"),
+                 ("salt", "<u4")])
+
+
+class GcmSA:
+    def __init__(self, rng, klen=16, esn=False, spi=None):
+        self.key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+        self.salt = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+        self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
+        self.esn = esn
+        self.oracle = O.SA(O.CSP_MODE_AEAD, self.key, self.salt,
+                           flags=O.CSP_F_SEPARATE_AAD if esn else 0)
+
+
+class EtaSA:
+    def __init__(self, rng, klen=32, esn=False, spi=None):
+        self.key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+        self.akey = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+        self.salt = b"\0\0\0\0"
+        self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
+        self.esn = esn
+        self.oracle = O.SA(O.CSP_MODE_ETA, self.key, akey=self.akey, mlen=12,
+                           flags=O.CSP_F_ESN if esn else 0)
+
+
+def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None):
+    """Plaintext ESP records + oracle-encrypted copies in one arena.
+
+    Returns (arena_plain, arena_ct, descs, esn_hi) as numpy arrays; records are
+    placed at 4-byte aligned offsets (stride_pad adds slack between records).
+    """
+    n = len(sa_idx)
+    hlen = 16 if gcm else 24
+    alen = 16 if gcm else 12
+    lens = np.array([hlen + int(c) + alen for c in ct_lens], dtype=np.int64)
+    offs = np.zeros(n, dtype=np.int64)
+    pos = 0
+    for i in range(n):
+        offs[i] = pos
+        pos += ((lens[i] + 3) & ~3) + stride_pad
+    arena = np.zeros(pos + 64, dtype=np.uint8)
+    if esn_hi is None:
+        esn_hi = np.zeros(n, dtype=np.uint32)
+    payload = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    for i in range(n):
+        sa = sas[sa_idx[i]]
+        o, L = offs[i], lens[i]
+        rec = arena[o:o + L]
+        rec[:] = payload[o:o + L]
+        rec[0:4] = np.frombuffer(sa.spi.to_bytes(4, "big"), dtype=np.uint8)
+        rec[4:8] = np.frombuffer(int(i + 1).to_bytes(4, "big"), dtype=np.uint8)
+        rec[L - alen:] = 0
+    descs = np.zeros(n, dtype=DESC)
+    descs["off4"] = offs // 4
+    descs["len"] = lens
+    descs["sa"] = sa_idx
+    descs["esn_hi"] = esn_hi
+    descs["salt"] = [int.from_bytes(sas[s].salt, "little") for s in sa_idx]
+    plain = arena.copy()
+    ct = arena.copy()
+    _, _ = O.batch([s.oracle for s in sas], ct, descs["off4"], descs["len"], descs["sa"],
+                   esn_hi=esn_hi, nthreads=8, encrypt=True)
+    return plain, ct, descs, esn_hi
+
+
+def oracle_decrypt(sas, arena, descs, esn_hi):
+    out = arena.copy()
+    _, st = O.batch([s.oracle for s in sas], out, descs["off4"], descs["len"], descs["sa"],
+                    esn_hi=esn_hi, nthreads=8)
+    return out, st

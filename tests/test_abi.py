@@ -1,0 +1,90 @@
+"""CPU tests of the drop-in boundary: libespgpu.so loads, exports every
+function include/espgpu.h declares, its structs have the ABI layout, and the
+host-only driver logic (probesession = swcr_probesession + check_csp for the
+ESP ciphers) answers like the reference.  No compute calls: no GPU here."""
+import ctypes as C
+
+import pytest
+
+from espgpu import _lib as L
+from espgpu.esp import CBC_SHA1, GCM, SecAssoc, esp_pad, esp_trailer_ok
+from espgpu.opencrypto import GpuCryptoDriver, crypto_session_params
+
+
+def test_library_exports_header_symbols():
+    lib = L.lib()
+    syms = L.header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), "missing export %s" % s
+    assert lib.espgpu_abi_version() == 1
+
+
+def test_struct_layouts():
+    assert C.sizeof(L.Desc) == 16
+    assert C.sizeof(L.Completion) == 16
+    assert L.Req.crp_iv.offset % 1 == 0
+    # espgpu_req must match the C layout: check a few offsets against natural alignment
+    assert L.Req.segs.offset == 16 and L.Req.crp_aad.offset == 32
+
+
+def _probe(**kw):
+    return GpuCryptoDriver.probesession(crypto_session_params(**kw))
+
+
+@pytest.mark.parametrize("klen", [16, 24, 32])
+def test_probesession_accepts_esp_gcm(klen):
+    assert _probe(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16,
+                  csp_cipher_klen=klen, csp_cipher_key=b"k" * klen) == L.CRYPTODEV_PROBE_HARDWARE
+    assert _probe(csp_mode=L.CSP_MODE_AEAD, csp_flags=L.CSP_F_SEPARATE_AAD, csp_ivlen=12,
+                  csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16, csp_cipher_klen=klen,
+                  csp_cipher_key=b"k" * klen) == L.CRYPTODEV_PROBE_HARDWARE
+
+
+def test_probesession_accepts_esp_cbc_sha1():
+    assert _probe(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=L.CRYPTO_AES_CBC,
+                  csp_cipher_klen=32, csp_cipher_key=b"k" * 32, csp_auth_alg=L.CRYPTO_SHA1_HMAC,
+                  csp_auth_klen=20, csp_auth_key=b"a" * 20, csp_auth_mlen=12) == -100
+
+
+@pytest.mark.parametrize("kw", [
+    dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=16, csp_cipher_alg=25, csp_cipher_klen=16),   # ivlen != 12
+    dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=25, csp_cipher_klen=20),   # bad key length
+    dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=11, csp_cipher_klen=16),   # CBC as AEAD
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=25, csp_cipher_klen=16,
+         csp_auth_alg=7, csp_auth_klen=20),                                                 # GCM as ETA
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
+         csp_auth_alg=9, csp_auth_klen=32),                                                 # SHA2 not served
+    dict(csp_mode=2, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16),                  # cipher-only
+    dict(csp_mode=L.CSP_MODE_AEAD, csp_flags=0x1, csp_ivlen=12, csp_cipher_alg=25,
+         csp_cipher_klen=16),                                                               # SEPARATE_OUTPUT
+])
+def test_probesession_rejects(kw):
+    assert _probe(**kw) == L.EINVAL
+
+
+def test_sa_session_params_follow_esp_init():
+    sa = SecAssoc(0x1234, GCM, bytes(20))
+    csp = sa.csp()
+    assert csp.csp_cipher_klen == 16 and csp.csp_ivlen == 12 and csp.csp_mode == L.CSP_MODE_AEAD
+    sa2 = SecAssoc(0x1234, CBC_SHA1, bytes(32), bytes(20), esn=True)
+    c2 = sa2.csp()
+    assert c2.csp_flags == L.CSP_F_ESN and c2.csp_auth_mlen == 12 and sa2.hlen == 24 and sa2.alen == 12
+
+
+def test_esp_padding_and_trailer_checks():
+    for n in range(40, 60):
+        p = esp_pad(bytes(n), blocksize=4)
+        assert len(p) % 4 == 0 and esp_trailer_ok(p)
+    p = bytearray(esp_pad(bytes(41), 16))
+    assert len(p) % 16 == 0
+    p[-2] = 200
+    assert not esp_trailer_ok(p)
+
+
+def test_init_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        GpuCryptoDriver()

@@ -1,0 +1,136 @@
+"""CPU tests: the oracle against the reference's own known answers.
+
+* DPDK ESP packet KATs (outer IP | ESP | IV | CT | ICV) decrypt to the expected
+  inner packet + padding, and a flipped ICV bit gives EBADMSG with the record
+  untouched (the esp_input_cb EBADMSG path, xform_esp.c:537-545).
+* DPDK AES-GCM AEAD KATs (128/192/256-bit keys, AAD 0..65296 bytes).
+* DPDK AES-CBC + HMAC-SHA1 chained KATs (digest over ciphertext, 12-byte trunc).
+* AES and GF(2^128) arithmetic against the reference's own rijndael-alg-fst.c
+  and gfmult.c compiled from /root/reference (oracle/_ref; skipped where the
+  reference tree is absent, e.g. on the GPU box).
+"""
+import hashlib
+import hmac
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import GcmSA, EtaSA, build_records, golden, oracle_decrypt
+
+
+@pytest.mark.parametrize("v", golden("esp_packets.json"), ids=lambda v: v["name"])
+def test_esp_packet_kat(v):
+    sa = O.SA(O.CSP_MODE_AEAD, bytes.fromhex(v["key"]), bytes.fromhex(v["salt"]))
+    rec = bytes.fromhex(v["esp_record"])
+    e, out = sa.esp_decrypt(rec)
+    assert e == 0
+    inner = bytes.fromhex(v["inner_packet"])
+    pt = out[16:len(out) - 16]
+    assert pt[:len(inner)] == inner
+    padlen, nh = pt[-2], pt[-1]
+    assert len(pt) == len(inner) + padlen + 2
+    assert pt[len(inner):len(inner) + padlen] == bytes(range(1, padlen + 1))
+    assert nh == (4 if inner[0] >> 4 == 4 else 41)
+    # re-encrypt gives back the KAT ciphertext and ICV
+    e2, again = sa.esp_encrypt(out)
+    assert e2 == 0 and again == rec
+    # corrupt one ICV bit: EBADMSG, buffer unchanged
+    bad = bytearray(rec)
+    bad[-1] ^= 0x01
+    e3, out3 = sa.esp_decrypt(bytes(bad))
+    assert e3 == O.EBADMSG and out3 == bytes(bad)
+
+
+def _aad(v):
+    aad = bytes.fromhex(v["aad"])
+    if v.get("aad_fill") == "repeat32":
+        aad = (aad * (v["aad_len"] // 32 + 1))[: v["aad_len"]]
+    return aad
+
+
+@pytest.mark.parametrize("v", golden("gcm_aead.json"), ids=lambda v: v["name"])
+def test_gcm_aead_kat(v):
+    key, iv = bytes.fromhex(v["key"]), bytes.fromhex(v["iv"])
+    e, ct, tag = O.gcm(key, iv, _aad(v), bytes.fromhex(v["plaintext"]))
+    assert e == 0 and ct.hex() == v["ciphertext"] and tag.hex() == v["tag"]
+    e, pt, _ = O.gcm(key, iv, _aad(v), bytes.fromhex(v["ciphertext"]), bytes.fromhex(v["tag"]),
+                     encrypt=False)
+    assert e == 0 and pt.hex() == v["plaintext"]
+
+
+@pytest.mark.parametrize("v", golden("cbc_hmac_sha1.json"), ids=lambda v: v["name"])
+def test_cbc_hmac_sha1_kat(v):
+    ak = bytes.fromhex(v.get("auth_key", "00"))
+    e, ct, dg = O.eta(bytes.fromhex(v["cipher_key"]), ak, bytes.fromhex(v["iv"]), b"",
+                      bytes.fromhex(v["plaintext"]))
+    assert e == 0 and ct.hex() == v["ciphertext"]
+    if "digest" in v:
+        assert dg.hex() == v["digest"]
+        e, pt, _ = O.eta(bytes.fromhex(v["cipher_key"]), ak, bytes.fromhex(v["iv"]), b"", ct,
+                         bytes.fromhex(v["digest"]), mlen=v["truncated_len"], encrypt=False)
+        assert e == 0 and pt.hex() == v["plaintext"]
+        bad = bytearray(bytes.fromhex(v["digest"]))
+        bad[0] ^= 0x80
+        e, pt, _ = O.eta(bytes.fromhex(v["cipher_key"]), ak, bytes.fromhex(v["iv"]), b"", ct,
+                         bytes(bad), mlen=v["truncated_len"], encrypt=False)
+        assert e == O.EBADMSG
+
+
+def test_sha1_hmac_against_hashlib():
+    rng = np.random.default_rng(7)
+    for n in (0, 1, 55, 56, 63, 64, 65, 119, 1000, 1464):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert O.sha1(m) == hashlib.sha1(m).digest()
+        k = rng.integers(0, 256, n % 90, dtype=np.uint8).tobytes()
+        assert O.hmac_sha1(k, m) == hmac.new(k, m, "sha1").digest()
+
+
+needs_ref = pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built (no /root/reference)")
+
+
+@needs_ref
+@pytest.mark.parametrize("klen", [16, 24, 32])
+def test_aes_against_reference_rijndael(klen):
+    rng = np.random.default_rng(klen)
+    for _ in range(200):
+        k = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        r, nr, rk = O.ref_aes_encrypt_block(k, b)
+        assert r == O.aes_encrypt_block(k, b) and (nr, rk) == O.aes_round_keys(k)
+        r, nr, rk = O.ref_aes_encrypt_block(k, b, decrypt=True)
+        assert r == O.aes_decrypt_block(k, b) and (nr, rk) == O.aes_round_keys(k, True)
+
+
+@needs_ref
+def test_gf128_against_reference_gfmult():
+    rng = np.random.default_rng(3)
+    for _ in range(500):
+        h = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        x = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        assert O.ref_gf128_mul(h, x) == O.gf128_mul(h, x)
+
+
+@pytest.mark.parametrize("gcm", [True, False])
+def test_oracle_batch_roundtrip(gcm):
+    """Batch driver: encrypt -> decrypt restores the plaintext; ICV flips -> EBADMSG."""
+    rng = np.random.default_rng(11)
+    sas = [GcmSA(rng) if gcm else EtaSA(rng) for _ in range(3)]
+    n = 64
+    sa_idx = rng.integers(0, 3, n)
+    cts = rng.choice([16, 48, 1440] if not gcm else [12, 204, 1448, 100], n)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, gcm=gcm)
+    bad = ct.copy()
+    for i in range(0, n, 5):
+        end = descs["off4"][i] * 4 + descs["len"][i]
+        bad[end - 1] ^= 1
+    out, st = oracle_decrypt(sas, bad, descs, eh)
+    for i in range(n):
+        o, L = descs["off4"][i] * 4, descs["len"][i]
+        alen = 16 if gcm else 12
+        if i % 5 == 0:
+            assert st[i] == O.EBADMSG and (out[o:o + L] == bad[o:o + L]).all()
+        else:
+            assert st[i] == 0
+            h = 16 if gcm else 24
+            assert (out[o + h:o + L - alen] == plain[o + h:o + L - alen]).all()
