@@ -19,11 +19,11 @@
 //    is no shift/reduce step: X*H^e = XOR_j T_e[j][nib_j(X)].  Each 256-byte
 //    position table spans all 64 LDS banks once, so a ds_read_b128 lookup is
 //    bank-conflict-free whatever the nibble values.
-//  * AES-CTR uses one T-table of (Te0[x], Te1[x]) pairs replicated 32x in LDS
-//    (entry x at x*256, lane slot (lane&31)*8): ds_read_b64 with every lane of a
-//    32-lane group on its own bank pair -> conflict-free; the LDS address is a
-//    single v_perm_b32 of (state byte, lane slot).  Te2/Te3 are folded through
-//    one ror16 per column: t = Te0[a]^Te1[b]^ror16(Te0[c]^Te1[d]^ror16(rk)).
+//  * AES-CTR uses T-tables Te0 and Te1 replicated 32x in LDS (entry x at x*256:
+//    Te0 in lane slots (lane&31)*4, Te1 128 bytes later): ds_read_b32 with every
+//    lane of a 32-lane group on its own bank -> conflict-free; the LDS address
+//    is a single v_perm_b32 of (state byte, lane slot).  Te2/Te3 are folded
+//    through one ror16 per column: t = Te0[a]^Te1[b]^ror16(Te0[c]^Te1[d]^ror16(rk)).
 //  * The lane that owns GHASH block i also computes AES(nonce||i+1): block 0
 //    (the AAD block) gets J0, CT block c = i-1 gets counter c+2, so the CTR
 //    work is perfectly aligned with the hash work and plaintext is stored from
@@ -102,54 +102,58 @@ __device__ __forceinline__ void st_partial(uint8_t *p, uint4 v, int rem) {
 
 // ---- AES (rijndaelEncrypt, rijndael-alg-fst.c:863-1042) on the pair table ----
 
-// LDS byte address of the pair for byte k of w: byte0 = lane slot, byte1 = w.byte k.
+// T-table layout (64 KiB): entry x occupies 256 bytes = Te0[x] replicated in
+// 32 lane slots (bytes 0..127) followed by Te1[x] = ror8(Te0[x]) in 32 slots
+// (bytes 128..255).  Lane L reads slot L&31, so for ds_read_b32 (32 banks,
+// bank = dword index mod 32, 32-lane groups) every lane of a group hits its
+// own bank whatever the indices: conflict-free.  The address of Te0[byte k of
+// w] for this lane is ONE v_perm_b32: byte0 = (L&31)*4, byte1 = w.byte k; Te1
+// is the same address + 128 (DS immediate offset).
 __device__ __forceinline__ uint32_t tpa(uint32_t w, uint32_t slot, int k) {
   return perm(w, slot, 0x0c0c0000u | ((4u + (uint32_t)k) << 8));
 }
+__device__ __forceinline__ uint32_t te0(const uint8_t *lds, uint32_t a) {
+  return *reinterpret_cast<const uint32_t *>(lds + a);
+}
+__device__ __forceinline__ uint32_t te1(const uint8_t *lds, uint32_t a) {
+  return *reinterpret_cast<const uint32_t *>(lds + a + 128);
+}
 
-template <int NR>
-__device__ __forceinline__ uint4 aes_enc(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+__device__ __forceinline__ uint4 aes_enc(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, int nr,
                                          const uint8_t *lds, uint32_t slot) {
-  // s* are big-endian state words already XORed with rk[0..3].
+  // s* are big-endian state words already XORed with rk[0..3].  nr is
+  // wave-uniform (one session per chunk): one loop body serves AES-128/192/256.
   const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LDS_RK);
-#pragma unroll
-  for (int r = 1; r < NR; ++r) {
+#pragma unroll 1
+  for (int r = 1; r < nr; ++r) {
     uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * r);
-    uint2 a0 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 3));
-    uint2 b0 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 2));
-    uint2 c0 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 1));
-    uint2 d0 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 0));
-    uint2 a1 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 3));
-    uint2 b1 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 2));
-    uint2 c1 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 1));
-    uint2 d1 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 0));
-    uint2 a2 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 3));
-    uint2 b2 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 2));
-    uint2 c2 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 1));
-    uint2 d2 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 0));
-    uint2 a3 = *reinterpret_cast<const uint2 *>(lds + tpa(s3, slot, 3));
-    uint2 b3 = *reinterpret_cast<const uint2 *>(lds + tpa(s0, slot, 2));
-    uint2 c3 = *reinterpret_cast<const uint2 *>(lds + tpa(s1, slot, 1));
-    uint2 d3 = *reinterpret_cast<const uint2 *>(lds + tpa(s2, slot, 0));
-    s0 = xor3(a0.x, b0.y, ror16(xor3(c0.x, d0.y, k.x)));
-    s1 = xor3(a1.x, b1.y, ror16(xor3(c1.x, d1.y, k.y)));
-    s2 = xor3(a2.x, b2.y, ror16(xor3(c2.x, d2.y, k.z)));
-    s3 = xor3(a3.x, b3.y, ror16(xor3(c3.x, d3.y, k.w)));
+    // column c: Te0[s_c.b3] ^ Te1[s_c+1.b2] ^ ror16(Te0[s_c+2.b1] ^ Te1[s_c+3.b0] ^ ror16(rk))
+    const uint32_t a0 = te0(lds, tpa(s0, slot, 3)), b0 = te1(lds, tpa(s1, slot, 2));
+    const uint32_t c0 = te0(lds, tpa(s2, slot, 1)), d0 = te1(lds, tpa(s3, slot, 0));
+    const uint32_t a1 = te0(lds, tpa(s1, slot, 3)), b1 = te1(lds, tpa(s2, slot, 2));
+    const uint32_t c1 = te0(lds, tpa(s3, slot, 1)), d1 = te1(lds, tpa(s0, slot, 0));
+    const uint32_t a2 = te0(lds, tpa(s2, slot, 3)), b2 = te1(lds, tpa(s3, slot, 2));
+    const uint32_t c2 = te0(lds, tpa(s0, slot, 1)), d2 = te1(lds, tpa(s1, slot, 0));
+    const uint32_t a3 = te0(lds, tpa(s3, slot, 3)), b3 = te1(lds, tpa(s0, slot, 2));
+    const uint32_t c3 = te0(lds, tpa(s1, slot, 1)), d3 = te1(lds, tpa(s2, slot, 0));
+    s0 = xor3(a0, b0, ror16(xor3(c0, d0, k.x)));
+    s1 = xor3(a1, b1, ror16(xor3(c1, d1, k.y)));
+    s2 = xor3(a2, b2, ror16(xor3(c2, d2, k.z)));
+    s3 = xor3(a3, b3, ror16(xor3(c3, d3, k.w)));
     __builtin_amdgcn_sched_barrier(0);
   }
   // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
   // words directly; the last round key is stored byte-swapped.
-  uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * NR);
-  const uint32_t *t32 = reinterpret_cast<const uint32_t *>(lds);
+  uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * nr);
   uint32_t a, b, c, d, o[4];
   uint32_t ss[4] = {s0, s1, s2, s3};
   uint32_t kk[4] = {k.x, k.y, k.z, k.w};
 #pragma unroll
   for (int col = 0; col < 4; ++col) {
-    a = t32[tpa(ss[col], slot, 3) >> 2];
-    b = t32[tpa(ss[(col + 1) & 3], slot, 2) >> 2];
-    c = t32[tpa(ss[(col + 2) & 3], slot, 1) >> 2];
-    d = t32[tpa(ss[(col + 3) & 3], slot, 0) >> 2];
+    a = te0(lds, tpa(ss[col], slot, 3));
+    b = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
+    c = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
+    d = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
     o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
@@ -157,27 +161,34 @@ __device__ __forceinline__ uint4 aes_enc(uint32_t s0, uint32_t s1, uint32_t s2, 
 
 // ---- GHASH multiply by a fixed power (gf128_mul, gfmult.c:219-229) ----------
 // pb = LDS byte address of the power's 8 KiB table (low byte 0, < 2^24).
+// Nibble position j = 8k + 2q (+1 for the high nibble) of word k, byte q.
 __device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds) {
   uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
+  // One 32-bit word (8 nibble positions) per iteration; the loop is kept
+  // rolled so at most 8 lookups (32 VGPRs) are in flight per wave, and the
+  // word in use is rotated into w instead of indexing an array (which would
+  // go to scratch).  pb advances 8 position tables (2 KiB) per word.
+  uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
+#pragma unroll 1
   for (int k = 0; k < 4; ++k) {
-    const uint32_t hi = w[k] & 0xF0F0F0F0u;           // high nibble * 16, per byte
-    const uint32_t lo = (w[k] << 4) & 0xF0F0F0F0u;    // low nibble * 16, per byte
+    const uint32_t hi = w & 0xF0F0F0F0u;           // high nibble * 16, per byte
+    const uint32_t lo = (w << 4) & 0xF0F0F0F0u;    // low nibble * 16, per byte
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t sel = 0x0c060500u | (uint32_t)q;
       const uint32_t alo = perm(pb, lo, sel);
       const uint32_t ahi = perm(pb, hi, sel);
-      const uint4 e = *reinterpret_cast<const uint4 *>(lds + alo + (8 * k + 2 * q) * 256);
-      const uint4 f = *reinterpret_cast<const uint4 *>(lds + ahi + (8 * k + 2 * q + 1) * 256);
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + alo + (2 * q) * 256);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + ahi + (2 * q + 1) * 256);
       r0 = xor3(r0, e.x, f.x);
       r1 = xor3(r1, e.y, f.y);
       r2 = xor3(r2, e.z, f.z);
       r3 = xor3(r3, e.w, f.w);
     }
-    // bound the lookahead to 8 lookups (32 VGPRs) so the hoisted loads do not spill
-    __builtin_amdgcn_sched_barrier(0);
+    w = w1;
+    w1 = w2;
+    w2 = w3;
+    pb += 8 * 256;
   }
   return make_uint4(r0, r1, r2, r3);
 }
@@ -196,41 +207,39 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
-template <int MODE, int NR>
-__device__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
-                         uint32_t sa, uint32_t sa_flags, uint32_t mlen) {
+template <int MODE>
+__device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di,
+                                                   bool have, uint32_t sa, uint32_t sa_flags,
+                                                   uint32_t mlen, int nr) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
-  const uint32_t slot = (uint32_t)(lane & 31) * 8;
+  const uint32_t slot = (uint32_t)(lane & 31) * 4;
   const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LDS_RK);
+  const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
 
   // -- descriptor and record header ------------------------------------------
   int valid = 0, ct_len = 0, nct = 0, N = 0, M = 0, pad = 0;
-  size_t base = 0;
-  uint32_t len = 0;
-  uint4 aadblk = make_uint4(0, 0, 0, 0), lenblk = make_uint4(0, 0, 0, 0);
+  uint8_t *rec = p.arena;
+  uint32_t len = 0, spi = 0, sn = 0, esnh = 0;
   uint32_t s0c = 0, s1c = 0, s2c = 0;
   if (have) {
     const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
-    base = (size_t)dv.x * 4;
     len = dv.y & 0xffffu;
-    const uint32_t dsa = dv.y >> 16;
-    ct_len = (int)len - 32;                        // 8 hdr + 8 IV + 16 ICV
-    valid = (dsa == sa) && ct_len > 0 && (len & 3) == 0;   // xform_esp.c:279-324
+    ct_len = (int)len - 32;                                  // 8 hdr + 8 IV + 16 ICV
+    valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;   // xform_esp.c:279-324
     if (valid) {
-      const uint2 hdr = *reinterpret_cast<const uint2 *>(p.arena + base);       // SPI, SN
-      const uint2 iv = *reinterpret_cast<const uint2 *>(p.arena + base + 8);    // explicit IV
-      const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
-      const uint32_t aad_len = sep ? 12 : 8;
-      aadblk = sep ? make_uint4(hdr.x, bswap32(dv.z), hdr.y, 0) : make_uint4(hdr.x, hdr.y, 0, 0);
-      lenblk = make_uint4(0, bswap32(aad_len * 8), 0, bswap32((uint32_t)ct_len * 8));
+      rec = p.arena + (size_t)dv.x * 4;
+      const uint4 h = ld16(rec);                             // SPI, SN, explicit IV
+      spi = h.x;
+      sn = h.y;
+      esnh = bswap32(dv.z);
       nct = (ct_len + 15) >> 4;
       N = nct + 2;
       M = (N + S - 1) / S;
       pad = S * M - N;
-      s0c = bswap32(dv.w) ^ rk[0];                 // salt
-      s1c = bswap32(iv.x) ^ rk[1];
-      s2c = bswap32(iv.y) ^ rk[2];
+      s0c = bswap32(dv.w) ^ rk[0];                           // salt
+      s1c = bswap32(h.z) ^ rk[1];
+      s2c = bswap32(h.w) ^ rk[2];
     }
   }
   int Mw = M;
@@ -241,16 +250,18 @@ __device__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bo
     return;
   }
   const uint32_t rk3 = rk[3];
-  uint8_t *rec = p.arena + base;
-  uint8_t *orec = (MODE == 0 ? p.out : p.arena) + base;
+  uint8_t *orec = (MODE == 0 ? p.out - p.arena + rec : rec);
 
   uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
   for (int m = 0; m < Mw; ++m) {
     const int i = S * m + l - pad;
-    if (m > 0) Y = gf_mul(Y, LDS_GT + 7 * 8192, lds);          // * H^8
+    if (m > 0) {
+      // * H^8; a record shorter than the wave's longest keeps its hash
+      const uint4 Yn = gf_mul(Y, LDS_GT + 7 * 8192, lds);
+      if (m < M) Y = Yn;
+    }
     uint4 ks = make_uint4(0, 0, 0, 0);
-    if (MODE != 2 || i == 0)
-      ks = aes_enc<NR>(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, lds, slot);
+    if (MODE != 2 || i == 0) ks = aes_enc(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, nr, lds, slot);
     uint4 B = make_uint4(0, 0, 0, 0);
     if (valid && i >= 1 && i <= nct) {
       const int c = i - 1;
@@ -264,11 +275,11 @@ __device__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bo
         B = mask_block(C, rem);
         if (MODE == 0) st_partial(orec + 16 + 16 * c, xor4(C, ks), rem);
       }
-    } else if (i == 0) {
-      B = aadblk;
+    } else if (valid && i == 0) {
+      B = sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0);     // AAD block
       EJ0 = ks;
-    } else if (i == N - 1) {
-      B = lenblk;
+    } else if (valid && i == N - 1) {
+      B = make_uint4(0, bswap32(sep ? 96u : 64u), 0, bswap32((uint32_t)ct_len * 8));   // len block
     }
     Y = xor4(Y, B);
   }
@@ -282,7 +293,7 @@ __device__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bo
 
   int ok = 1;
   if (valid) {
-    const size_t icv = len - 16;
+    const uint32_t icv = len - 16;
     if (MODE == 1) {
       if (l == 0) st_partial(rec + icv, T, (int)mlen);
     } else {
@@ -299,7 +310,7 @@ __device__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bo
     for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
     for (int m = 0; m < Mr; ++m) {
       const int i = S * m + l - pad;
-      const uint4 ks = aes_enc<NR>(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, lds, slot);
+      const uint4 ks = aes_enc(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, nr, lds, slot);
       if (run && i >= 1 && i <= nct) {
         const int c = i - 1;
         const uint4 C = ld16(rec + 16 + 16 * c);
@@ -316,10 +327,12 @@ __global__ __launch_bounds__(WG, 1) void gcm_kernel(GcmParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
 
-  // Pair table, replicated into 32 lane slots per entry.
+  // T-table: per entry 32 slots of Te0 then 32 slots of Te1 (see tpa()).
   for (int idx = tid; idx < 256 * 32; idx += WG) {
     const int x = idx >> 5, r = idx & 31;
-    *reinterpret_cast<uint2 *>(lds + LDS_TP + x * 256 + r * 8) = p.tpair[x];
+    const uint2 t = p.tpair[x];
+    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
+    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
   }
 
   const bool implicit = (p.chunks == nullptr);
@@ -369,12 +382,7 @@ __global__ __launch_bounds__(WG, 1) void gcm_kernel(GcmParams p) {
       if (have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
       continue;
     }
-    if (nr == 10)
-      do_group<MODE, 10>(p, lds, di, have, sa, flags, mlen);
-    else if (nr == 12)
-      do_group<MODE, 12>(p, lds, di, have, sa, flags, mlen);
-    else
-      do_group<MODE, 14>(p, lds, di, have, sa, flags, mlen);
+    do_group<MODE>(p, lds, di, have, sa, flags, mlen, (int)nr);
   }
 }
 

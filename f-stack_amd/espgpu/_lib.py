@@ -86,6 +86,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("libespgpu.so not found at %s: build it with "
                                "`make -C f-stack_amd` (hipcc, gfx950)" % LIB_PATH)
+        # One HIP runtime per process: torch bundles its own libamdhip64 (same
+        # soname, libamdhip64.so.7).  Loaded first, it satisfies our DT_NEEDED;
+        # loaded after us it would come in as a second runtime that sees no
+        # devices.  So bring torch in first when it is installed.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.espgpu_abi_version.restype = C.c_int

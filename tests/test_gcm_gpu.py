@@ -103,10 +103,16 @@ def test_opencrypto_encrypt_then_decrypt(fw):
         fw.crypto_drain()
         for pkt, ref in zip(pkts, refs):
             assert bytes(pkt[20:]) == ref
+        crps = []
         for pkt in pkts:
             crp = esp_input_crp(fw, ses, sa, pkt, 20)
+            crps.append(crp)
             assert fw.crypto_dispatch(crp) == 0
         fw.crypto_drain()
+        for crp, pkt, ref in zip(crps, pkts, refs):
+            assert crp.crp_etype == 0
+            e, dec = orc.esp_decrypt(ref)
+            assert bytes(pkt[20 + 16:-16]) == dec[16:-16]
         fw.crypto_freesession(ses)
 
 

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Collect the rocprofv3 evidence for one bench configuration (run ON the GPU box).
+#   tools/profile.sh <tag> [extra bench.py args]
+# Writes gpurun_out/prof_<tag>/{trace,pmc_fetch,pmc_write,pmc_sq}/ .  Counter
+# passes are separate runs with --kernel-trace only beside --pmc (never sys-trace).
+set -euo pipefail
+TAG=${1:?tag}; shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH=(python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu "$@")
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/trace.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_write.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_sq" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_sq.log" 2>&1
+echo "profile $TAG done"
