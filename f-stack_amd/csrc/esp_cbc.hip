@@ -1,8 +1,359 @@
-// esp_cbc.hip — ESP AES-CBC + HMAC-SHA1-96 (CSP_MODE_ETA) kernels.  (stub)
+// esp_cbc.hip — ESP AES-CBC + HMAC-SHA1-96 (CSP_MODE_ETA) kernels for gfx950.
+//
+// Replaces swcr_eta (freebsd/opencrypto/cryptosoft.c:874-888) =
+//   decrypt: swcr_authcompute (verify, :317-382) then swcr_encdec (CBC, :101-284)
+//   encrypt: swcr_encdec then swcr_authcompute (compute, ICV written)
+// for the request esp_input / esp_output build (xform_esp.c:296-461):
+//   AAD = ESP header + IV (hlen = 8 + 16 bytes), payload = CBC ciphertext,
+//   HMAC-SHA1 over AAD || payload (|| ESN high 32 bits, CSP_F_ESN), ICV = the
+//   first mlen (12) bytes, IV = the 16 bytes before the payload.
+//
+// Mapping: a wave owns 64 records.
+//  * HMAC-SHA1 is a serial chain per record, so lane = record: each lane runs
+//    its record's SHA-1 compressions from the precomputed ipad/opad chaining
+//    states (hmac_init_pad, crypto.c:413-441), 80 rounds fully unrolled in
+//    registers, no tables.
+//  * CBC decryption is block-parallel: the wave then walks its 64 records one
+//    at a time and all 64 lanes decrypt that record's blocks (P_i = D(C_i) ^
+//    C_{i-1}), 64 consecutive blocks per pass, last pass first, so in-place
+//    decryption never reads a block another lane already overwrote.  AES decryption uses Td0/Td1 tables replicated 32x in LDS
+//    (conflict-free ds_read_b32, one v_perm_b32 per address, as in esp_gcm.hip)
+//    and a replicated inverse S-box for the last round.
+//  * CBC encryption is serial per record (lane = record), Te0/Te1 in LDS.
 #include <hip/hip_runtime.h>
 
 #include "espgpu_internal.h"
 
 namespace espgpu {
-int launch_eta(const EtaParams &, int, int, void *) { return -1; }
+
+namespace {
+
+constexpr uint32_t LDS_T = 0;          // Td0/Td1 (decrypt) or Te0/Te1 (encrypt), 64 KiB
+constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32 KiB
+constexpr uint32_t LDS_BYTES = 65536 + 32768;
+
+typedef const __attribute__((address_space(4))) uint32_t *kptr;
+
+struct __attribute__((aligned(4))) U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t ror16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return perm(x, x, 0x00010203u); }
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+  U4 v = *reinterpret_cast<const U4 *>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
+  *reinterpret_cast<U4 *>(p) = U4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+__device__ __forceinline__ uint4 bswap4(uint4 v) {
+  return make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+}
+
+// T-table addressing, see esp_gcm.hip: entry x at x*256, T0 in lane slots
+// (lane&31)*4, T1 128 bytes later.
+__device__ __forceinline__ uint32_t tpa(uint32_t w, uint32_t slot, int k) {
+  return perm(w, slot, 0x0c0c0000u | ((4u + (uint32_t)k) << 8));
+}
+__device__ __forceinline__ uint32_t t0(const uint8_t *lds, uint32_t a) {
+  return *reinterpret_cast<const uint32_t *>(lds + a);
+}
+__device__ __forceinline__ uint32_t t1(const uint8_t *lds, uint32_t a) {
+  return *reinterpret_cast<const uint32_t *>(lds + a + 128);
+}
+
+// ---- AES decryption (rijndaelDecrypt, rijndael-alg-fst.c:1044-1222) --------
+// dk = rijndaelKeySetupDec schedule (big-endian words).  Input/output are
+// little-endian memory words.
+template <typename KP>
+__device__ __forceinline__ uint4 aes_dec(uint4 in, KP dk, int nr, const uint8_t *lds, uint32_t slot) {
+  uint32_t s0 = bswap32(in.x) ^ dk[0], s1 = bswap32(in.y) ^ dk[1];
+  uint32_t s2 = bswap32(in.z) ^ dk[2], s3 = bswap32(in.w) ^ dk[3];
+#pragma unroll 1
+  for (int r = 1; r < nr; ++r) {
+    const uint32_t k0 = ror16(dk[4 * r]), k1 = ror16(dk[4 * r + 1]);
+    const uint32_t k2 = ror16(dk[4 * r + 2]), k3 = ror16(dk[4 * r + 3]);
+    // t_c = Td0[s_c.b3] ^ Td1[s_c-1.b2] ^ ror16(Td0[s_c+2.b1] ^ Td1[s_c+1.b0] ^ ror16(rk))
+    const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s3, slot, 2));
+    const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s1, slot, 0));
+    const uint32_t a1 = t0(lds, tpa(s1, slot, 3)), b1 = t1(lds, tpa(s0, slot, 2));
+    const uint32_t c1 = t0(lds, tpa(s3, slot, 1)), d1 = t1(lds, tpa(s2, slot, 0));
+    const uint32_t a2 = t0(lds, tpa(s2, slot, 3)), b2 = t1(lds, tpa(s1, slot, 2));
+    const uint32_t c2 = t0(lds, tpa(s0, slot, 1)), d2 = t1(lds, tpa(s3, slot, 0));
+    const uint32_t a3 = t0(lds, tpa(s3, slot, 3)), b3 = t1(lds, tpa(s2, slot, 2));
+    const uint32_t c3 = t0(lds, tpa(s1, slot, 1)), d3 = t1(lds, tpa(s0, slot, 0));
+    s0 = xor3(a0, b0, ror16(xor3(c0, d0, k0)));
+    s1 = xor3(a1, b1, ror16(xor3(c1, d1, k1)));
+    s2 = xor3(a2, b2, ror16(xor3(c2, d2, k2)));
+    s3 = xor3(a3, b3, ror16(xor3(c3, d3, k3)));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // last round: Si bytes from the replicated inverse S-box (dword per entry)
+  const uint32_t *si = reinterpret_cast<const uint32_t *>(lds + LDS_SI);
+  const uint32_t ls = slot >> 2;
+  uint32_t ss[4] = {s0, s1, s2, s3}, o[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t a = si[((ss[c] >> 24) << 5) | ls];
+    const uint32_t b = si[(((ss[(c + 3) & 3] >> 16) & 0xff) << 5) | ls];
+    const uint32_t cc = si[(((ss[(c + 2) & 3] >> 8) & 0xff) << 5) | ls];
+    const uint32_t d = si[((ss[(c + 1) & 3] & 0xff) << 5) | ls];
+    o[c] = (a | (b << 8) | (cc << 16) | (d << 24)) ^ bswap32(dk[4 * nr + c]);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// ---- AES encryption (rijndaelEncrypt) with Te0/Te1 in LDS ------------------
+template <typename KP>
+__device__ __forceinline__ uint4 aes_enc(uint4 in, KP ek, int nr, const uint8_t *lds, uint32_t slot) {
+  uint32_t s0 = bswap32(in.x) ^ ek[0], s1 = bswap32(in.y) ^ ek[1];
+  uint32_t s2 = bswap32(in.z) ^ ek[2], s3 = bswap32(in.w) ^ ek[3];
+#pragma unroll 1
+  for (int r = 1; r < nr; ++r) {
+    const uint32_t k0 = ror16(ek[4 * r]), k1 = ror16(ek[4 * r + 1]);
+    const uint32_t k2 = ror16(ek[4 * r + 2]), k3 = ror16(ek[4 * r + 3]);
+    const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s1, slot, 2));
+    const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s3, slot, 0));
+    const uint32_t a1 = t0(lds, tpa(s1, slot, 3)), b1 = t1(lds, tpa(s2, slot, 2));
+    const uint32_t c1 = t0(lds, tpa(s3, slot, 1)), d1 = t1(lds, tpa(s0, slot, 0));
+    const uint32_t a2 = t0(lds, tpa(s2, slot, 3)), b2 = t1(lds, tpa(s3, slot, 2));
+    const uint32_t c2 = t0(lds, tpa(s0, slot, 1)), d2 = t1(lds, tpa(s1, slot, 0));
+    const uint32_t a3 = t0(lds, tpa(s3, slot, 3)), b3 = t1(lds, tpa(s0, slot, 2));
+    const uint32_t c3 = t0(lds, tpa(s1, slot, 1)), d3 = t1(lds, tpa(s2, slot, 0));
+    s0 = xor3(a0, b0, ror16(xor3(c0, d0, k0)));
+    s1 = xor3(a1, b1, ror16(xor3(c1, d1, k1)));
+    s2 = xor3(a2, b2, ror16(xor3(c2, d2, k2)));
+    s3 = xor3(a3, b3, ror16(xor3(c3, d3, k3)));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  uint32_t ss[4] = {s0, s1, s2, s3}, o[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t a = t0(lds, tpa(ss[c], slot, 3));
+    const uint32_t b = t0(lds, tpa(ss[(c + 1) & 3], slot, 2));
+    const uint32_t cc = t0(lds, tpa(ss[(c + 2) & 3], slot, 1));
+    const uint32_t d = t0(lds, tpa(ss[(c + 3) & 3], slot, 0));
+    o[c] = xor3(perm(b, a, 0x0c0c0501u), perm(d, cc, 0x05010c0cu), bswap32(ek[4 * nr + c]));
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// ---- SHA-1 compression (sha1_step, freebsd/crypto/sha1.c:94-176) ----------
+__device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+  for (int t = 0; t < 80; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+      w[t & 15] = wt;
+    }
+    uint32_t f, k;
+    if (t < 20) {
+      f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);   // (b & c) | (~b & d)
+      k = 0x5a827999u;
+    } else if (t < 40) {
+      f = xor3(b, c, d);
+      k = 0x6ed9eba1u;
+    } else if (t < 60) {
+      f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);   // majority
+      k = 0x8f1bbcdcu;
+    } else {
+      f = xor3(b, c, d);
+      k = 0xca62c1d6u;
+    }
+    const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+    e = d;
+    d = c;
+    c = rotl(b, 30);
+    b = a;
+    a = tmp;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// HMAC-SHA1 of msg = rec[0, L0) || (esn ? be32(esn_hi) : "") from the SA's
+// ipad/opad chaining states (already past the 64-byte key block).
+__device__ void hmac_sha1(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi,
+                          kptr ipad, kptr opad, uint32_t out[5]) {
+  const uint32_t L = L0 + (esn ? 4u : 0u);              // multiple of 4 for ESP records
+  const uint32_t nfull = L0 / 64;                       // blocks entirely from memory
+  const uint32_t total = (L + 9 + 63) / 64;             // inner blocks incl. padding
+  const uint64_t bits = (uint64_t)(64 + L) * 8;         // the ipad block counts
+  uint32_t h[5] = {ipad[0], ipad[1], ipad[2], ipad[3], ipad[4]};
+  uint32_t w[16];
+  // One compression site for every block (inner data, inner padding, outer)
+  // keeps a single inlined copy of the 80 rounds.
+  for (uint32_t b = 0; b <= total; ++b) {
+    if (b < nfull) {
+      const uint8_t *p = rec + 64 * b;
+      const uint4 q0 = bswap4(ld16(p)), q1 = bswap4(ld16(p + 16)), q2 = bswap4(ld16(p + 32)),
+                  q3 = bswap4(ld16(p + 48));
+      w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w;
+      w[4] = q1.x; w[5] = q1.y; w[6] = q1.z; w[7] = q1.w;
+      w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+      w[12] = q3.x; w[13] = q3.y; w[14] = q3.z; w[15] = q3.w;
+    } else if (b < total) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t o = 64 * b + 4 * k;
+        uint32_t v;
+        if (o + 4 <= L0) v = bswap32(*reinterpret_cast<const uint32_t *>(rec + o));
+        else if (esn && o == L0) v = esn_hi;
+        else if (o == L) v = 0x80000000u;
+        else v = 0;
+        if (b == total - 1 && k == 14) v = (uint32_t)(bits >> 32);
+        if (b == total - 1 && k == 15) v = (uint32_t)bits;
+        w[k] = v;
+      }
+    } else {
+      // outer: opad state, block = inner digest || 0x80 || 0... || (64+20)*8
+#pragma unroll
+      for (int k = 0; k < 5; ++k) w[k] = h[k];
+      w[5] = 0x80000000u;
+#pragma unroll
+      for (int k = 6; k < 15; ++k) w[k] = 0;
+      w[15] = (64 + 20) * 8;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) h[k] = opad[k];
+    }
+    sha1_compress(h, w);
+  }
+  for (int k = 0; k < 5; ++k) out[k] = h[k];
+}
+
+__device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
+
+// MODE 0: decrypt out-of-place; 1: encrypt in place; 2: decrypt in place (verify first)
+template <int MODE, int WG>
+__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t slot = (uint32_t)(lane & 31) * 4;
+  const uint2 *tab = MODE == 1 ? p.tpair : p.dpair;
+  for (int idx = tid; idx < 256 * 32; idx += WG) {
+    const int x = idx >> 5, r = idx & 31;
+    const uint2 t = tab[x];
+    *reinterpret_cast<uint32_t *>(lds + LDS_T + x * 256 + r * 4) = t.x;
+    *reinterpret_cast<uint32_t *>(lds + LDS_T + x * 256 + 128 + r * 4) = t.y;
+    if (MODE != 1) *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[x];
+  }
+  __syncthreads();
+
+  const uint32_t waves = gridDim.x * (WG / 64);
+  const uint32_t wave = blockIdx.x * (WG / 64) + (tid >> 6);
+  for (uint32_t base = wave * 64; base < p.n; base += waves * 64) {
+    // ---- lane = record: descriptor, HMAC (verify or compute) ----
+    const uint32_t di = base + lane;
+    bool have = di < p.n, valid = false, ok = false;
+    uint32_t off = 0, len = 0, sa = 0, plen = 0;
+    if (have) {
+      const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+      off = dv.x * 4;
+      len = dv.y & 0xffffu;
+      sa = dv.y >> 16;
+      const DevSA *s = sa < p.nsas ? p.sas + sa : nullptr;
+      if (!s || s->mode != ESPGPU_CSP_MODE_ETA) {
+        have = false;                                       // not ours (GCM kernel / EINVAL)
+        if (!s || s->mode == 0) p.status[di] = ESPGPU_EINVAL;
+      } else {
+        const uint32_t mlen = s->mlen;
+        const int pl = (int)len - 24 - (int)mlen;           // hlen 24, alen = mlen (12)
+        valid = pl > 0 && (pl & 15) == 0 && (len & 3) == 0;  // xform_esp.c:316-324
+        plen = valid ? (uint32_t)pl : 0;
+        if (valid && MODE != 1) {
+          uint32_t dg[5];
+          const uint8_t *rec = p.arena + off;
+          hmac_sha1(rec, 24 + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, dv.z, kp(s->ipad),
+                    kp(s->opad), dg);
+          uint32_t diff = 0;
+          for (uint32_t k = 0; k < mlen / 4; ++k)
+            diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + 24 + plen + 4 * k);
+          ok = diff == 0;
+        }
+      }
+    }
+    if (MODE == 1) {
+      // ---- encrypt: CBC chain is serial, lane = record ----
+      if (have && valid) {
+        const DevSA *s = p.sas + sa;
+        uint8_t *rec = p.arena + off;
+        uint4 prev = ld16(rec + 8);                         // IV
+        const int nr = (int)s->nr;
+        for (uint32_t b = 0; b < plen / 16; ++b) {
+          const uint4 c = aes_enc(xor4(ld16(rec + 24 + 16 * b), prev), s->rk, nr, lds, slot);
+          st16(rec + 24 + 16 * b, c);
+          prev = c;
+        }
+        uint32_t dg[5];
+        hmac_sha1(rec, 24 + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, p.desc[di].esn_hi,
+                  kp(s->ipad), kp(s->opad), dg);
+        for (uint32_t k = 0; k < s->mlen / 4; ++k)
+          *reinterpret_cast<uint32_t *>(rec + 24 + plen + 4 * k) = bswap32(dg[k]);
+      }
+      if (have) p.status[di] = valid ? ESPGPU_OK : ESPGPU_EINVAL;
+      continue;
+    }
+    if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+
+    // ---- decrypt: the wave walks its records; lanes split each record's blocks ----
+    const bool run_me = have && valid && (MODE == 0 || ok);
+    uint64_t todo = __ballot(run_me);
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t roff = __shfl(off, j), rplen = __shfl(plen, j), rsa = __shfl(sa, j);
+      const DevSA *s = p.sas + __builtin_amdgcn_readfirstlane(rsa);
+      const int nr = (int)s->nr;
+      const kptr dk = kp(s->dk);
+      const uint8_t *rec = p.arena + __builtin_amdgcn_readfirstlane(roff);
+      uint8_t *orec = (MODE == 0 ? p.out : p.arena) + __builtin_amdgcn_readfirstlane(roff);
+      const uint32_t nblk = __builtin_amdgcn_readfirstlane(rplen) / 16;
+      // Passes of 64 consecutive blocks, last pass first: within a pass every
+      // lane loads C_i and C_{i-1} before any lane stores, and a pass only
+      // overwrites blocks that no later (lower) pass reads, so in-place
+      // decryption is safe without holding the record in registers.
+      for (int pb = (int)((nblk - 1) & ~63u); pb >= 0; pb -= 64) {
+        const uint32_t i = (uint32_t)pb + lane;
+        if (i < nblk) {
+          const uint4 c = ld16(rec + 24 + 16 * i);
+          const uint4 prev = ld16(rec + 8 + 16 * i);         // C_{i-1}, or the IV for i = 0
+          const uint4 pt = xor4(aes_dec(c, dk, nr, lds, slot), prev);
+          st16(orec + 24 + 16 * i, pt);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// Decrypt runs 512-thread workgroups (2 waves/SIMD, up to 256 VGPRs: the
+// unrolled SHA-1 schedule needs ~170 and spills at 128); encrypt runs 1024.
+int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (grid <= 0) grid = 256;
+  const int two_pass = !encrypt && p.out == p.arena;
+  if (encrypt)
+    hipLaunchKernelGGL((eta_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, p);
+  else if (two_pass)
+    hipLaunchKernelGGL((eta_kernel<2, 512>), dim3(grid), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL((eta_kernel<0, 512>), dim3(grid), dim3(512), 0, st, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 }  // namespace espgpu

@@ -41,10 +41,13 @@ namespace {
 
 constexpr uint32_t LDS_TP = 0;          // 256 entries x 32 lane slots x 8 B
 constexpr uint32_t LDS_GT = 65536;      // 8 powers x 32 positions x 16 x 16 B
-constexpr uint32_t LDS_RK = 131072;     // 64 words round keys (kernel form)
-constexpr uint32_t LDS_BYTES = LDS_RK + 64 * 4;
-constexpr int WG = 1024;
+constexpr uint32_t LDS_BYTES = 131072;
 constexpr int S = 8;                    // lanes per record
+
+// Round keys are read through the constant address space: uniform loads from
+// it become s_load (SGPRs, scalar cache) instead of vector loads or LDS reads.
+typedef const __attribute__((address_space(4))) uint32_t *rkptr;
+__device__ __forceinline__ uint4 ldk4(rkptr p) { return make_uint4(p[0], p[1], p[2], p[3]); }
 
 struct __attribute__((aligned(4))) U4 {
   uint32_t x, y, z, w;
@@ -52,6 +55,14 @@ struct __attribute__((aligned(4))) U4 {
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// Same operation as an opaque asm: LLVM may not reassociate across it, which
+// keeps each GHASH lookup group's XOR folding next to its loads (otherwise the
+// XOR chain is re-associated to the end and every lookup result stays live).
+__device__ __forceinline__ uint32_t xor3_pin(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
   return __builtin_amdgcn_perm(hi, lo, sel);
@@ -119,44 +130,122 @@ __device__ __forceinline__ uint32_t te1(const uint8_t *lds, uint32_t a) {
   return *reinterpret_cast<const uint32_t *>(lds + a + 128);
 }
 
-__device__ __forceinline__ uint4 aes_enc(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, int nr,
-                                         const uint8_t *lds, uint32_t slot) {
-  // s* are big-endian state words already XORed with rk[0..3].  nr is
-  // wave-uniform (one session per chunk): one loop body serves AES-128/192/256.
-  const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LDS_RK);
-#pragma unroll 1
-  for (int r = 1; r < nr; ++r) {
-    uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * r);
-    // column c: Te0[s_c.b3] ^ Te1[s_c+1.b2] ^ ror16(Te0[s_c+2.b1] ^ Te1[s_c+3.b0] ^ ror16(rk))
-    const uint32_t a0 = te0(lds, tpa(s0, slot, 3)), b0 = te1(lds, tpa(s1, slot, 2));
-    const uint32_t c0 = te0(lds, tpa(s2, slot, 1)), d0 = te1(lds, tpa(s3, slot, 0));
-    const uint32_t a1 = te0(lds, tpa(s1, slot, 3)), b1 = te1(lds, tpa(s2, slot, 2));
-    const uint32_t c1 = te0(lds, tpa(s3, slot, 1)), d1 = te1(lds, tpa(s0, slot, 0));
-    const uint32_t a2 = te0(lds, tpa(s2, slot, 3)), b2 = te1(lds, tpa(s3, slot, 2));
-    const uint32_t c2 = te0(lds, tpa(s0, slot, 1)), d2 = te1(lds, tpa(s1, slot, 0));
-    const uint32_t a3 = te0(lds, tpa(s3, slot, 3)), b3 = te1(lds, tpa(s0, slot, 2));
-    const uint32_t c3 = te0(lds, tpa(s1, slot, 1)), d3 = te1(lds, tpa(s2, slot, 0));
-    s0 = xor3(a0, b0, ror16(xor3(c0, d0, k.x)));
-    s1 = xor3(a1, b1, ror16(xor3(c1, d1, k.y)));
-    s2 = xor3(a2, b2, ror16(xor3(c2, d2, k.z)));
-    s3 = xor3(a3, b3, ror16(xor3(c3, d3, k.w)));
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
-  // words directly; the last round key is stored byte-swapped.
-  uint4 k = *reinterpret_cast<const uint4 *>(rk + 4 * nr);
+// One middle round on big-endian state words; k = ror16(round key) (kernel form).
+__device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint4 k,
+                                          const uint8_t *lds, uint32_t slot) {
+  // column c: Te0[s_c.b3] ^ Te1[s_c+1.b2] ^ ror16(Te0[s_c+2.b1] ^ Te1[s_c+3.b0] ^ ror16(rk))
+  const uint32_t a0 = te0(lds, tpa(s0, slot, 3)), b0 = te1(lds, tpa(s1, slot, 2));
+  const uint32_t c0 = te0(lds, tpa(s2, slot, 1)), d0 = te1(lds, tpa(s3, slot, 0));
+  const uint32_t a1 = te0(lds, tpa(s1, slot, 3)), b1 = te1(lds, tpa(s2, slot, 2));
+  const uint32_t c1 = te0(lds, tpa(s3, slot, 1)), d1 = te1(lds, tpa(s0, slot, 0));
+  const uint32_t a2 = te0(lds, tpa(s2, slot, 3)), b2 = te1(lds, tpa(s3, slot, 2));
+  const uint32_t c2 = te0(lds, tpa(s0, slot, 1)), d2 = te1(lds, tpa(s1, slot, 0));
+  const uint32_t a3 = te0(lds, tpa(s3, slot, 3)), b3 = te1(lds, tpa(s0, slot, 2));
+  const uint32_t c3 = te0(lds, tpa(s1, slot, 1)), d3 = te1(lds, tpa(s2, slot, 0));
+  s0 = xor3(a0, b0, ror16(xor3(c0, d0, k.x)));
+  s1 = xor3(a1, b1, ror16(xor3(c1, d1, k.y)));
+  s2 = xor3(a2, b2, ror16(xor3(c2, d2, k.z)));
+  s3 = xor3(a3, b3, ror16(xor3(c3, d3, k.w)));
+}
+
+// S-box copy in global memory for the experimental L1-gather last round
+// (variant bit 2): spreads lookups over the vector-memory path as well as LDS.
+__device__ uint8_t g_sbox[256];
+__device__ uint32_t g_opts;   // bit0: L1-gather last round
+
+// Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
+// words directly; the last round key is stored byte-swapped.
+template <bool LASTG>
+__device__ __forceinline__ uint4 aes_last(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint4 k,
+                                          const uint8_t *lds, uint32_t slot) {
   uint32_t a, b, c, d, o[4];
   uint32_t ss[4] = {s0, s1, s2, s3};
   uint32_t kk[4] = {k.x, k.y, k.z, k.w};
 #pragma unroll
   for (int col = 0; col < 4; ++col) {
-    a = te0(lds, tpa(ss[col], slot, 3));
-    b = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
-    c = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
-    d = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
-    o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
+    if (LASTG) {
+      a = g_sbox[ss[col] >> 24];
+      b = g_sbox[(ss[(col + 1) & 3] >> 16) & 0xff];
+      c = g_sbox[(ss[(col + 2) & 3] >> 8) & 0xff];
+      d = g_sbox[ss[(col + 3) & 3] & 0xff];
+      o[col] = (a | (b << 8) | (c << 16) | (d << 24)) ^ kk[col];
+    } else {
+      a = te0(lds, tpa(ss[col], slot, 3));
+      b = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
+      c = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
+      d = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
+      o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
+    }
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Rounds r0..nr-1 (middle) and the last round.  s* = state entering round r0.
+__device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, int r0,
+                                            int nr, rkptr rk, const uint8_t *lds,
+                                            uint32_t slot) {
+  // nr and rk are wave-uniform (one session per chunk): one loop body serves
+  // AES-128/192/256, and the round keys come in through scalar loads (SGPRs),
+  // not LDS, which is the bottleneck resource.
+#pragma unroll 1
+  for (int r = r0; r < nr; ++r) {
+    aes_round(s0, s1, s2, s3, ldk4(rk + 4 * r), lds, slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (*(rkptr)(const void *)&g_opts & 1)
+    return aes_last<true>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
+  return aes_last<false>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
+}
+
+// ---- counter-mode caching of rounds 1-2 ------------------------------------
+// Every counter block of a record is nonce(12 B) || ctr, and within a run of
+// 256 counters only ctr's low byte changes.  Entering round 1 that byte is
+// s3.b0, which feeds exactly one T-table lookup (column 0); after round 1 only
+// column 0 (t0) varies, and in round 2 each output column has exactly one
+// lookup on t0.  So for a fixed nonce and ctr>>8 the other 15 + 12 lookups are
+// constants: K0 (round 1, column 0 without its s3.b0 term) and L0..L3 (round 2
+// without their t0 terms).  Per block this leaves 1 + 4 lookups for rounds 1-2
+// instead of 32 (the whole AES-128 block: 133 LDS lookups instead of 160).
+struct CtrCache {
+  uint32_t K0, L0, L1, L2, L3;
+  int hi;
+};
+
+__device__ __forceinline__ void ctr_cache_build(CtrCache &cc, uint32_t s0, uint32_t s1, uint32_t s2,
+                                                int hi, rkptr rk, const uint8_t *lds,
+                                                uint32_t slot) {
+  const uint32_t s3 = ((uint32_t)hi << 8) ^ rk[3];   // bytes 1..3 valid; byte 0 varies
+  const uint4 k1 = ldk4(rk + 4);
+  const uint4 k2 = ldk4(rk + 8);
+  // round 1 (k1 = ror16(rk[4..7]))
+  cc.K0 = xor3(te0(lds, tpa(s0, slot, 3)), te1(lds, tpa(s1, slot, 2)),
+               ror16(te0(lds, tpa(s2, slot, 1)) ^ k1.x));
+  const uint32_t t1 = xor3(te0(lds, tpa(s1, slot, 3)), te1(lds, tpa(s2, slot, 2)),
+                           ror16(xor3(te0(lds, tpa(s3, slot, 1)), te1(lds, tpa(s0, slot, 0)), k1.y)));
+  const uint32_t t2 = xor3(te0(lds, tpa(s2, slot, 3)), te1(lds, tpa(s3, slot, 2)),
+                           ror16(xor3(te0(lds, tpa(s0, slot, 1)), te1(lds, tpa(s1, slot, 0)), k1.z)));
+  const uint32_t t3 = xor3(te0(lds, tpa(s3, slot, 3)), te1(lds, tpa(s0, slot, 2)),
+                           ror16(xor3(te0(lds, tpa(s1, slot, 1)), te1(lds, tpa(s2, slot, 0)), k1.w)));
+  __builtin_amdgcn_sched_barrier(0);
+  // round 2, each column without its t0 lookup
+  cc.L0 = te1(lds, tpa(t1, slot, 2)) ^ ror16(xor3(te0(lds, tpa(t2, slot, 1)), te1(lds, tpa(t3, slot, 0)), k2.x));
+  cc.L1 = xor3(te0(lds, tpa(t1, slot, 3)), te1(lds, tpa(t2, slot, 2)),
+               ror16(te0(lds, tpa(t3, slot, 1)) ^ k2.y));
+  cc.L2 = xor3(te0(lds, tpa(t2, slot, 3)), te1(lds, tpa(t3, slot, 2)),
+               ror16(te1(lds, tpa(t1, slot, 0)) ^ k2.z));
+  cc.L3 = te0(lds, tpa(t3, slot, 3)) ^ ror16(xor3(te0(lds, tpa(t1, slot, 1)), te1(lds, tpa(t2, slot, 0)), k2.w));
+  cc.hi = hi;
+}
+
+// E_K(nonce || ctr) using the cache (which must be built for ctr >> 8).
+__device__ __forceinline__ uint4 aes_ctr(const CtrCache &cc, uint32_t ctr, uint32_t rk3, int nr,
+                                         rkptr rk, const uint8_t *lds, uint32_t slot) {
+  const uint32_t t0 = cc.K0 ^ ror16(te1(lds, tpa(ctr ^ rk3, slot, 0)));
+  const uint32_t v0 = cc.L0 ^ te0(lds, tpa(t0, slot, 3));
+  const uint32_t v1 = cc.L1 ^ ror16(te1(lds, tpa(t0, slot, 0)));
+  const uint32_t v2 = cc.L2 ^ ror16(te0(lds, tpa(t0, slot, 1)));
+  const uint32_t v3 = cc.L3 ^ te1(lds, tpa(t0, slot, 2));
+  return aes_rounds(v0, v1, v2, v3, 3, nr, rk, lds, slot);
 }
 
 // ---- GHASH multiply by a fixed power (gf128_mul, gfmult.c:219-229) ----------
@@ -193,6 +282,54 @@ __device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds
   return make_uint4(r0, r1, r2, r3);
 }
 
+// 8 lookups of one 32-bit word (nibble positions 8k..8k+7), accumulated into r*.
+__device__ __forceinline__ void gf_group(uint32_t w, uint32_t pb, uint32_t &r0, uint32_t &r1,
+                                         uint32_t &r2, uint32_t &r3, const uint8_t *lds) {
+  const uint32_t hi = w & 0xF0F0F0F0u, lo = (w << 4) & 0xF0F0F0F0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t sel = 0x0c060500u | (uint32_t)q;
+    const uint4 e = *reinterpret_cast<const uint4 *>(lds + perm(pb, lo, sel) + (2 * q) * 256);
+    const uint4 f = *reinterpret_cast<const uint4 *>(lds + perm(pb, hi, sel) + (2 * q + 1) * 256);
+    r0 = xor3_pin(r0, e.x, f.x);
+    r1 = xor3_pin(r1, e.y, f.y);
+    r2 = xor3_pin(r2, e.z, f.z);
+    r3 = xor3_pin(r3, e.w, f.w);
+  }
+}
+
+// One pipeline step of a lane: E_K(nonce||ctr) and, when GH, Y <- Y * H^8.
+// The two are independent, so each GHASH word group is issued in the same
+// LDS batch as an AES round: the wave waits on 9 dependent LDS round trips per
+// step instead of 13, and the LDS sees 16-24 lookups per batch.
+template <bool GH>
+__device__ __forceinline__ uint4 ctr_ghash_step(const CtrCache &cc, uint32_t ctr, uint32_t rk3, int nr,
+                                                uint4 &Y, rkptr rk, const uint8_t *lds,
+                                                uint32_t slot) {
+  const uint32_t pb = LDS_GT + 7 * 8192;                  // H^8
+  uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0;
+  // rounds 1-2 from the counter cache (1 + 4 lookups) || GHASH word 0
+  if (GH) gf_group(Y.x, pb, g0, g1, g2, g3, lds);
+  const uint32_t t0 = cc.K0 ^ ror16(te1(lds, tpa(ctr ^ rk3, slot, 0)));
+  uint32_t s0 = cc.L0 ^ te0(lds, tpa(t0, slot, 3));
+  uint32_t s1 = cc.L1 ^ ror16(te1(lds, tpa(t0, slot, 0)));
+  uint32_t s2 = cc.L2 ^ ror16(te0(lds, tpa(t0, slot, 1)));
+  uint32_t s3 = cc.L3 ^ te1(lds, tpa(t0, slot, 2));
+  __builtin_amdgcn_sched_barrier(0);
+  // rounds 3-5 || GHASH words 1-3
+  if (GH) gf_group(Y.y, pb + 2048, g0, g1, g2, g3, lds);
+  aes_round(s0, s1, s2, s3, ldk4(rk + 12), lds, slot);
+  __builtin_amdgcn_sched_barrier(0);
+  if (GH) gf_group(Y.z, pb + 4096, g0, g1, g2, g3, lds);
+  aes_round(s0, s1, s2, s3, ldk4(rk + 16), lds, slot);
+  __builtin_amdgcn_sched_barrier(0);
+  if (GH) gf_group(Y.w, pb + 6144, g0, g1, g2, g3, lds);
+  aes_round(s0, s1, s2, s3, ldk4(rk + 20), lds, slot);
+  __builtin_amdgcn_sched_barrier(0);
+  if (GH) Y = make_uint4(g0, g1, g2, g3);
+  return aes_rounds(s0, s1, s2, s3, 6, nr, rk, lds, slot);
+}
+
 __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
   return make_uint4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m), __shfl_xor(v.w, m));
 }
@@ -207,14 +344,13 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
-template <int MODE>
+template <int MODE, bool FUSE>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di,
                                                    bool have, uint32_t sa, uint32_t sa_flags,
-                                                   uint32_t mlen, int nr) {
+                                                   uint32_t mlen, int nr, rkptr rk) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
-  const uint32_t *rk = reinterpret_cast<const uint32_t *>(lds + LDS_RK);
   const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
 
   // -- descriptor and record header ------------------------------------------
@@ -251,17 +387,28 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   }
   const uint32_t rk3 = rk[3];
   uint8_t *orec = (MODE == 0 ? p.out - p.arena + rec : rec);
+  CtrCache cc;
+  cc.hi = -1;                                               // built on first use
 
   uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
   for (int m = 0; m < Mw; ++m) {
     const int i = S * m + l - pad;
-    if (m > 0) {
-      // * H^8; a record shorter than the wave's longest keeps its hash
-      const uint4 Yn = gf_mul(Y, LDS_GT + 7 * 8192, lds);
-      if (m < M) Y = Yn;
-    }
+    const uint32_t ctr = i >= 0 ? (uint32_t)(i + 1) : 1u;     // J0 for block 0, c+2 for CT c
+    if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
     uint4 ks = make_uint4(0, 0, 0, 0);
-    if (MODE != 2 || i == 0) ks = aes_enc(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, nr, lds, slot);
+    if (MODE != 2 && FUSE) {
+      // keystream || Y * H^8 (a record shorter than the wave's longest keeps its hash)
+      uint4 Yn = Y;
+      ks = (m > 0) ? ctr_ghash_step<true>(cc, ctr, rk3, nr, Yn, rk, lds, slot)
+                   : ctr_ghash_step<false>(cc, ctr, rk3, nr, Yn, rk, lds, slot);
+      if (m < M) Y = Yn;
+    } else {
+      if (m > 0) {
+        const uint4 Yn = gf_mul(Y, LDS_GT + 7 * 8192, lds);
+        if (m < M) Y = Yn;
+      }
+      if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
+    }
     uint4 B = make_uint4(0, 0, 0, 0);
     if (valid && i >= 1 && i <= nct) {
       const int c = i - 1;
@@ -310,7 +457,9 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
     for (int m = 0; m < Mr; ++m) {
       const int i = S * m + l - pad;
-      const uint4 ks = aes_enc(s0c, s1c, s2c, (uint32_t)(i + 1) ^ rk3, nr, lds, slot);
+      const uint32_t ctr = i >= 0 ? (uint32_t)(i + 1) : 1u;
+      if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
+      const uint4 ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
       if (run && i >= 1 && i <= nct) {
         const int c = i - 1;
         const uint4 C = ld16(rec + 16 + 16 * c);
@@ -322,8 +471,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
-template <int MODE>
-__global__ __launch_bounds__(WG, 1) void gcm_kernel(GcmParams p) {
+template <int MODE, int WG, bool FUSE>
+__global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
 
@@ -367,36 +516,63 @@ __global__ __launch_bounds__(WG, 1) void gcm_kernel(GcmParams p) {
         uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
 #pragma unroll 4
         for (int q = tid; q < (int)(kGhTableBytes / 16); q += WG) dst[q] = src[q];
-        if (tid < 64) reinterpret_cast<uint32_t *>(lds + LDS_RK)[tid] = s->rk[tid];
       } else {
         mode = 0;
       }
       cur_sa = sa;
       __syncthreads();
     }
-    const uint32_t rl = (uint32_t)wave * S + ((tid & 63) >> 3);
-    const bool have = rl < count;
-    const uint32_t pos = start + (have ? rl : 0);
-    const uint32_t di = p.order ? p.order[pos] : pos;
-    if (mode != ESPGPU_CSP_MODE_AEAD) {
-      if (have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
-      continue;
+    // a 128-record chunk takes 128 / (WG/8) passes of the workgroup
+    for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * S) {
+      const uint32_t rl = sub + (uint32_t)wave * S + ((tid & 63) >> 3);
+      const bool have = rl < count;
+      const uint32_t pos = start + (have ? rl : 0);
+      const uint32_t di = p.order ? p.order[pos] : pos;
+      if (mode != ESPGPU_CSP_MODE_AEAD) {
+        // no session: EINVAL; an ETA session's records belong to the ETA kernel
+        if (mode == 0 && have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
+        continue;
+      }
+      do_group<MODE, FUSE>(p, lds, di, have, sa, flags, mlen, (int)nr,
+                           (rkptr)(const void *)(p.sas[sa].rk));
     }
-    do_group<MODE>(p, lds, di, have, sa, flags, mlen, (int)nr);
   }
 }
 
 }  // namespace
 
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream) {
+// variant: bit0 = 512-thread workgroups (2 waves/SIMD, 256 VGPRs) instead of
+// 1024 (4 waves/SIMD, 128 VGPRs); bit1 = fuse GHASH word groups into AES rounds.
+template <int MODE>
+static void launch_mode(const GcmParams &p, int variant, int grid, hipStream_t st) {
+  switch (variant & 3) {
+    case 0: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, false>), dim3(grid), dim3(1024), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((gcm_kernel<MODE, 512, false>), dim3(grid), dim3(512), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true>), dim3(grid), dim3(1024), 0, st, p); break;
+    default: hipLaunchKernelGGL((gcm_kernel<MODE, 512, true>), dim3(grid), dim3(512), 0, st, p); break;
+  }
+}
+
+int gcm_set_sbox(const uint8_t *sbox256) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sbox), sbox256, 256) == hipSuccess ? 0 : -1;
+}
+
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  static int cur_opts = -1;
+  const uint32_t opts = (variant >> 2) & 1;
+  if ((int)opts != cur_opts) {
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_opts), &opts, 4, 0, hipMemcpyHostToDevice, st);
+    hipStreamSynchronize(st);
+    cur_opts = (int)opts;
+  }
   if (grid <= 0) grid = 256;
   if (encrypt)
-    hipLaunchKernelGGL(gcm_kernel<1>, dim3(grid), dim3(WG), 0, st, p);
+    launch_mode<1>(p, variant, grid, st);
   else if (two_pass)
-    hipLaunchKernelGGL(gcm_kernel<2>, dim3(grid), dim3(WG), 0, st, p);
+    launch_mode<2>(p, variant, grid, st);
   else
-    hipLaunchKernelGGL(gcm_kernel<0>, dim3(grid), dim3(WG), 0, st, p);
+    launch_mode<0>(p, variant, grid, st);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -87,6 +88,7 @@ struct espgpu_ctx {
   std::vector<espgpu_completion> ready;   // host-side completions (EINVAL etc.)
   espgpu_stats stats{};
   float last_ms = 0.f;
+  int gcm_variant = 0;       // tuning: see launch_gcm
   std::string err;
 };
 
@@ -199,7 +201,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st)) return fail(c, EIO, "GCM kernel launch failed");
+  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, c->gcm_variant, st)) return fail(c, EIO, "GCM kernel launch failed");
   if (c->n_eta > 0) {
     EtaParams q{};
     q.arena = d_arena;
@@ -237,6 +239,7 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
   if (!cfg.nbatches) cfg.nbatches = 2;
   c->cfg = cfg;
   c->device = cfg.device;
+  if (const char *v = getenv("ESPGPU_GCM_VARIANT")) c->gcm_variant = atoi(v);
   int rc = 0;
   do {
     int ndev = 0;
@@ -266,6 +269,7 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     hipMemcpy(c->d_tpair, tp, sizeof tp, hipMemcpyHostToDevice);
     hipMemcpy(c->d_dpair, dp, sizeof dp, hipMemcpyHostToDevice);
     hipMemcpy(c->d_isbox, t.isbox, 256, hipMemcpyHostToDevice);
+    gcm_set_sbox(t.sbox);
     c->slots.resize(cfg.nbatches);
     for (auto &s : c->slots)
       if ((rc = alloc_slot(c, s))) break;
@@ -585,5 +589,12 @@ int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_d
 }
 
 float espgpu_last_kernel_ms(espgpu_ctx *c) { return c ? c->last_ms : 0.f; }
+
+int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
+  if (!c || !key) return EINVAL;
+  if (!strcmp(key, "gcm_variant")) { c->gcm_variant = value; return 0; }
+  if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
+  return ENOENT;
+}
 
 }  // extern "C"

@@ -74,7 +74,8 @@ struct EtaParams {
 };
 
 // Launchers (defined in the .hip files, called by espgpu.cpp).
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream);
+int gcm_set_sbox(const uint8_t *sbox256);
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream);
 int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,

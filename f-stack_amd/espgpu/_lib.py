@@ -115,6 +115,7 @@ def lib():
         L.espgpu_encrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp]
         L.espgpu_last_kernel_ms.argtypes = [vp]
         L.espgpu_last_kernel_ms.restype = C.c_float
+        L.espgpu_set_tuning.argtypes = [vp, C.c_char_p, C.c_int]
         _lib = L
     return _lib
 

@@ -180,6 +180,11 @@ int  espgpu_encrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu
  * batch stream), for the roofline accounting in bench.py. */
 float espgpu_last_kernel_ms(espgpu_ctx *ctx);
 
+/* Tuning knobs (engine-internal, for A/B measurement): "gcm_variant"
+ * (bit0: 512-thread workgroups, bit1: GHASH/AES round fusion), "grid"
+ * (workgroups per launch, 0 = 256).  Returns 0 or ENOENT. */
+int  espgpu_set_tuning(espgpu_ctx *ctx, const char *key, int value);
+
 #ifdef __cplusplus
 }
 #endif

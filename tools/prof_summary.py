@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/<tag>.json (+ pmc_<cfg>.json).
+
+  python tools/prof_summary.py gpurun_out/prof_<tag> <tag> [cfg]
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced read (16 B/lane loads), so it is doubled; WRITE_SIZE is exact for
+16-B/lane stores.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_stats(d):
+    out = {}
+    p = os.path.join(d, "trace", "run_kernel_stats.csv")
+    for r in csv.DictReader(open(p)):
+        out[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                          "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
+                          "pct": float(r["Percentage"])}
+    return out
+
+
+def counters(d, sub, match):
+    p = os.path.join(d, sub, "run_counter_collection.csv")
+    if not os.path.exists(p):
+        return {}
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(p)):
+        if match in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    cfg = sys.argv[3] if len(sys.argv) > 3 else "cfg1"
+    ks = kernel_stats(d)
+    dominant = max(ks, key=lambda k: ks[k]["pct"])
+    key = "gcm_kernel<0>" if "gcm_kernel<0>" in dominant else dominant
+    c = {}
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        c.update(counters(d, sub, key))
+    res = {"tag": tag, "config": cfg, "dominant_kernel": dominant, "kernels": ks, "counters": c}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rd = 2 * c["FETCH_SIZE"] * 1024
+        wr = c["WRITE_SIZE"] * 1024
+        res["hbm_read_bytes_per_launch"] = rd
+        res["hbm_write_bytes_per_launch"] = wr
+        res["hbm_bytes_per_launch"] = rd + wr
+    if "GRBM_GUI_ACTIVE" in c:
+        res["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / ks[dominant]["avg_ns"]
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "%s.json" % tag), "w") as f:
+        json.dump(res, f, indent=1)
+    if "hbm_bytes_per_launch" in res:
+        with open(os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg), "w") as f:
+            json.dump({"source": "profiles/%s.json" % tag,
+                       "hbm_bytes_per_launch": round(res["hbm_bytes_per_launch"])}, f, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    print("dominant:", dominant, ks[dominant])
+
+
+if __name__ == "__main__":
+    main()
