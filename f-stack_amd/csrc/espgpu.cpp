@@ -60,7 +60,7 @@ struct Slot {
   uint8_t *h_status = nullptr, *d_status = nullptr;
   uint32_t nrec = 0, bytes = 0;
   std::vector<Pending> reqs;
-  hipEvent_t done = nullptr;
+  hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
 };
 
 }  // namespace
@@ -68,8 +68,16 @@ struct Slot {
 struct espgpu_ctx {
   int device = 0;
   espgpu_config cfg{};
-  hipStream_t stream = nullptr;
+  // three streams so that batch k+1's H2D, batch k's kernels and batch k-1's
+  // D2H overlap: stream (compute), s_in (host->device), s_out (device->host)
+  hipStream_t stream = nullptr, s_in = nullptr, s_out = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // host-to-host pipeline (espgpu_decrypt_host) device mirrors
+  uint8_t *e2e_arena = nullptr, *e2e_out = nullptr, *e2e_status = nullptr;
+  espgpu_desc *e2e_desc = nullptr;
+  uint64_t e2e_bytes = 0;
+  uint32_t e2e_n = 0;
+  hipEvent_t e2e_in[2] = {nullptr, nullptr}, e2e_k[2] = {nullptr, nullptr};
   DevSA *d_sas = nullptr;
   uint8_t *d_gtab = nullptr;
   uint2 *d_tpair = nullptr, *d_dpair = nullptr;
@@ -166,13 +174,17 @@ int alloc_slot(espgpu_ctx *c, Slot &s) {
   HIPCHK(c, hipMalloc(&s.d_desc, recs * sizeof(espgpu_desc)));
   HIPCHK(c, hipMalloc(&s.d_status, recs));
   HIPCHK(c, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  HIPCHK(c, hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming));
+  HIPCHK(c, hipEventCreate(&s.k0));
+  HIPCHK(c, hipEventCreate(&s.k1));
   return 0;
 }
 
 void free_slot(Slot &s) {
   hipHostFree(s.h_arena); hipHostFree(s.h_desc); hipHostFree(s.h_status);
   hipFree(s.d_arena); hipFree(s.d_out); hipFree(s.d_desc); hipFree(s.d_status);
-  if (s.done) hipEventDestroy(s.done);
+  for (hipEvent_t e : {s.done, s.in_done, s.k0, s.k1})
+    if (e) hipEventDestroy(e);
 }
 
 // Launch the crypto kernels for one batch of device-resident records.
@@ -248,7 +260,16 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
       break;
     }
     if (hipSetDevice(cfg.device) != hipSuccess) { rc = fail(c, ENODEV, "hipSetDevice failed"); break; }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = fail(c, EIO, "stream"); break; }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
+      rc = fail(c, EIO, "stream");
+      break;
+    }
+    for (int k = 0; k < 2; ++k) {
+      hipEventCreateWithFlags(&c->e2e_in[k], hipEventDisableTiming);
+      hipEventCreateWithFlags(&c->e2e_k[k], hipEventDisableTiming);
+    }
     hipEventCreate(&c->ev0);
     hipEventCreate(&c->ev1);
     if (hipMalloc(&c->d_sas, (size_t)cfg.max_sessions * sizeof(DevSA)) != hipSuccess ||
@@ -285,13 +306,20 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
 
 void espgpu_fini(espgpu_ctx *c) {
   if (!c) return;
-  if (c->stream) hipStreamSynchronize(c->stream);
+  for (hipStream_t st : {c->s_in, c->stream, c->s_out})
+    if (st) hipStreamSynchronize(st);
   for (auto &s : c->slots) free_slot(s);
+  hipFree(c->e2e_arena); hipFree(c->e2e_out); hipFree(c->e2e_status); hipFree(c->e2e_desc);
+  for (int k = 0; k < 2; ++k) {
+    if (c->e2e_in[k]) hipEventDestroy(c->e2e_in[k]);
+    if (c->e2e_k[k]) hipEventDestroy(c->e2e_k[k]);
+  }
   hipFree(c->d_sas); hipFree(c->d_gtab); hipFree(c->d_tpair); hipFree(c->d_dpair); hipFree(c->d_isbox);
   hipFree(c->d_work); hipFree(c->d_order); hipFree(c->d_chunks); hipFree(c->d_nchunks);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
-  if (c->stream) hipStreamDestroy(c->stream);
+  for (hipStream_t st : {c->s_in, c->stream, c->s_out})
+    if (st) hipStreamDestroy(st);
   delete c;
 }
 
@@ -383,6 +411,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   if (!c || sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return;
   // Records already flushed keep their results; wait so the slot is not reused under them.
   hipStreamSynchronize(c->stream);
+  hipStreamSynchronize(c->s_out);
   if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
   c->sessions[sid] = Session();
   DevSA z;
@@ -500,16 +529,20 @@ int espgpu_flush(espgpu_ctx *c) {
   if (!c) return EINVAL;
   Slot &s = c->slots[c->cur];
   if (s.state != SLOT_FILLING || s.nrec == 0) return 0;
-  hipStream_t st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(s.d_arena, s.h_arena, s.bytes + 16, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(s.d_desc, s.h_desc, s.nrec * sizeof(espgpu_desc), hipMemcpyHostToDevice, st));
-  hipEventRecord(c->ev0, st);
-  int e = run_batch(c, s.d_arena, s.d_desc, s.nrec, s.d_status, s.op ? nullptr : s.d_out, 0, s.op, st);
+  // H2D on s_in -> kernels on the compute stream -> D2H on s_out, chained by
+  // events, so consecutive batches overlap their copies with each other's kernels.
+  HIPCHK(c, hipMemcpyAsync(s.d_arena, s.h_arena, s.bytes + 16, hipMemcpyHostToDevice, c->s_in));
+  HIPCHK(c, hipMemcpyAsync(s.d_desc, s.h_desc, s.nrec * sizeof(espgpu_desc), hipMemcpyHostToDevice, c->s_in));
+  HIPCHK(c, hipEventRecord(s.in_done, c->s_in));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, s.in_done, 0));
+  hipEventRecord(s.k0, c->stream);
+  int e = run_batch(c, s.d_arena, s.d_desc, s.nrec, s.d_status, s.op ? nullptr : s.d_out, 0, s.op, c->stream);
   if (e) return e;
-  hipEventRecord(c->ev1, st);
-  HIPCHK(c, hipMemcpyAsync(s.h_arena, s.op ? s.d_arena : s.d_out, s.bytes, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(s.h_status, s.d_status, s.nrec, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipEventRecord(s.done, st));
+  hipEventRecord(s.k1, c->stream);
+  HIPCHK(c, hipStreamWaitEvent(c->s_out, s.k1, 0));
+  HIPCHK(c, hipMemcpyAsync(s.h_arena, s.op ? s.d_arena : s.d_out, s.bytes, hipMemcpyDeviceToHost, c->s_out));
+  HIPCHK(c, hipMemcpyAsync(s.h_status, s.d_status, s.nrec, hipMemcpyDeviceToHost, c->s_out));
+  HIPCHK(c, hipEventRecord(s.done, c->s_out));
   s.state = SLOT_INFLIGHT;
   c->stats.batches++;
   c->cur = (c->cur + 1) % (int)c->slots.size();
@@ -518,7 +551,7 @@ int espgpu_flush(espgpu_ctx *c) {
 
 static int complete_slot(espgpu_ctx *c, Slot &s) {
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) {
+  if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) {
     c->last_ms = ms;
     c->stats.kernel_ns += (uint64_t)(ms * 1e6);
   }
@@ -563,7 +596,7 @@ int espgpu_drain(espgpu_ctx *c) {
   if (!c) return EINVAL;
   int e = espgpu_flush(c);
   if (e) return e;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->s_out));
   for (auto &s : c->slots)
     if (s.state == SLOT_INFLIGHT) complete_slot(c, s);
   return 0;
@@ -589,6 +622,57 @@ int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_d
 }
 
 float espgpu_last_kernel_ms(espgpu_ctx *c) { return c ? c->last_ms : 0.f; }
+
+static int host_pipeline(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_bytes,
+                         const espgpu_desc *h_desc, uint32_t n, uint8_t *h_status, uint8_t *h_out,
+                         uint32_t chunk, uint32_t flags, int encrypt) {
+  if (!c || !h_arena || !h_desc || !h_status || (!encrypt && !h_out)) return EINVAL;
+  if (n == 0) return 0;
+  if (!chunk) chunk = 65536;
+  if (arena_bytes + 64 > c->e2e_bytes || n > c->e2e_n) {
+    hipFree(c->e2e_arena); hipFree(c->e2e_out); hipFree(c->e2e_status); hipFree(c->e2e_desc);
+    c->e2e_bytes = arena_bytes + 64;
+    c->e2e_n = n;
+    HIPCHK(c, hipMalloc(&c->e2e_arena, c->e2e_bytes));
+    HIPCHK(c, hipMalloc(&c->e2e_out, c->e2e_bytes));
+    HIPCHK(c, hipMalloc(&c->e2e_status, n));
+    HIPCHK(c, hipMalloc(&c->e2e_desc, (size_t)n * sizeof(espgpu_desc)));
+  }
+  // Chunks of consecutive records (descriptors in ascending arena order) map to
+  // contiguous byte ranges, copied to the same offsets of a device mirror so the
+  // descriptors are used unchanged.
+  for (uint32_t i0 = 0, k = 0; i0 < n; i0 += chunk, ++k) {
+    const uint32_t i1 = std::min(n, i0 + chunk), m = i1 - i0;
+    uint64_t lo = (uint64_t)h_desc[i0].off4 * 4, hi = 0;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint64_t o = (uint64_t)h_desc[i].off4 * 4;
+      lo = std::min(lo, o);
+      hi = std::max(hi, o + h_desc[i].len);
+    }
+    hi = std::min(arena_bytes, hi + 16);                 // partial-block loads read <= 16 B past
+    hipEvent_t ein = c->e2e_in[k & 1], ek = c->e2e_k[k & 1];
+    HIPCHK(c, hipMemcpyAsync(c->e2e_desc + i0, h_desc + i0, m * sizeof(espgpu_desc), hipMemcpyHostToDevice, c->s_in));
+    HIPCHK(c, hipMemcpyAsync(c->e2e_arena + lo, h_arena + lo, hi - lo, hipMemcpyHostToDevice, c->s_in));
+    HIPCHK(c, hipEventRecord(ein, c->s_in));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, ein, 0));
+    int e = run_batch(c, c->e2e_arena, c->e2e_desc + i0, m, c->e2e_status + i0,
+                      encrypt ? nullptr : c->e2e_out, flags, encrypt, c->stream);
+    if (e) return e;
+    HIPCHK(c, hipEventRecord(ek, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->s_out, ek, 0));
+    uint8_t *dst = encrypt ? (uint8_t *)h_arena : h_out;
+    HIPCHK(c, hipMemcpyAsync(dst + lo, (encrypt ? c->e2e_arena : c->e2e_out) + lo, hi - lo, hipMemcpyDeviceToHost, c->s_out));
+    HIPCHK(c, hipMemcpyAsync(h_status + i0, c->e2e_status + i0, m, hipMemcpyDeviceToHost, c->s_out));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->s_out));
+  return 0;
+}
+
+int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_bytes,
+                        const espgpu_desc *h_desc, uint32_t n, uint8_t *h_status, uint8_t *h_out,
+                        uint32_t chunk, uint32_t flags) {
+  return host_pipeline(c, h_arena, arena_bytes, h_desc, n, h_status, h_out, chunk, flags, 0);
+}
 
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return EINVAL;

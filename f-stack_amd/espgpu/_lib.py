@@ -116,6 +116,8 @@ def lib():
         L.espgpu_last_kernel_ms.argtypes = [vp]
         L.espgpu_last_kernel_ms.restype = C.c_float
         L.espgpu_set_tuning.argtypes = [vp, C.c_char_p, C.c_int]
+        L.espgpu_decrypt_host.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, vp, vp, C.c_uint32,
+                                          C.c_uint32]
         _lib = L
     return _lib
 

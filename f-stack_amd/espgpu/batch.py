@@ -46,3 +46,16 @@ def encrypt_batch(driver, arena, desc, n, status, grouped=False, stream=None):
         L.BATCH_GROUPED if grouped else 0, _stream_ptr(stream))
     if rc:
         raise RuntimeError("espgpu_encrypt_batch: %s" % driver.last_error())
+
+
+def decrypt_host(driver, arena, desc, n, status, out, chunk=0, flags=0):
+    """Host-to-host pipelined decrypt (espgpu_decrypt_host): arena/desc/status/out
+    are pinned CPU tensors (torch .pin_memory()); the engine streams chunks
+    through HBM with H2D, kernels and D2H overlapped on three HIP streams."""
+    for t in (arena, desc, status, out):
+        assert not t.is_cuda and t.is_contiguous() and t.is_pinned()
+    rc = driver.lib.espgpu_decrypt_host(
+        driver.ctx, arena.data_ptr(), arena.numel(), desc.data_ptr(), n, status.data_ptr(),
+        out.data_ptr(), chunk, flags)
+    if rc:
+        raise RuntimeError("espgpu_decrypt_host: %s" % driver.last_error())

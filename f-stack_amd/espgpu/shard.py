@@ -33,3 +33,23 @@ def spis_for_rank(rank, ngpus, count, start=0x100):
             out.append(s)
         s += 1
     return out
+
+
+def random_spis(count, seed):
+    """`count` distinct random SPIs >= 256 (SPIs 1..255 are reserved, RFC 4303 2.1)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = set()
+    while len(out) < count:
+        out.update(int(x) for x in rng.integers(256, 2**32, count - len(out), dtype=np.uint64))
+    return sorted(out)
+
+
+def shard_plan(spis, sa_of_packet, rank, ngpus):
+    """SPI-hash partition of a global batch: (local SA indices, local packet
+    indices) owned by `rank`.  Every packet goes where its SA's SPI hashes."""
+    import numpy as np
+    owner = np.array([gpu_of_spi(s, ngpus) for s in spis], dtype=np.int64)
+    local_sas = np.nonzero(owner == rank)[0]
+    local_pkts = np.nonzero(owner[np.asarray(sa_of_packet)] == rank)[0]
+    return local_sas, local_pkts

@@ -149,7 +149,8 @@ void espgpu_freesession(espgpu_ctx *ctx, int32_t session);
  * then sets cc_qblocked and requeues, crypto.c:1451-1459).  Malformed requests
  * complete with crp_etype = EINVAL via poll(), as crypto_done would. */
 int  espgpu_process(espgpu_ctx *ctx, const struct espgpu_req *req, int hint);
-/* Launch everything staged so far (H2D, kernels, D2H on the ctx stream).
+/* Launch everything staged so far: H2D, kernels and D2H on three ctx streams
+ * chained by events, so consecutive batches overlap copies with kernels.
  * F-Stack's main_loop calls this once per RX burst (lib/ff_dpdk_if.c:2363). */
 int  espgpu_flush(espgpu_ctx *ctx);
 /* Complete finished requests: copies results back into the caller's segments
@@ -175,6 +176,16 @@ int  espgpu_decrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu
                           void *stream);
 int  espgpu_encrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
                           uint32_t n, uint8_t *d_status, uint32_t flags, void *stream);
+
+/* Host-to-host pipelined decrypt of a large host-resident batch (the shape of
+ * an offload from DPDK hugepage mbufs): records in h_arena (pinned: hipHostMalloc
+ * or hipHostRegister), descriptors in ascending arena order; `chunk` records per
+ * step (0 = 65536).  Step k's H2D, step k-1's kernels and step k-2's D2H run
+ * concurrently on three HIP streams.  Plaintext lands in h_out at the same
+ * offsets; returns when everything is back. */
+int  espgpu_decrypt_host(espgpu_ctx *ctx, const uint8_t *h_arena, uint64_t arena_bytes,
+                         const struct espgpu_desc *h_desc, uint32_t n, uint8_t *h_status,
+                         uint8_t *h_out, uint32_t chunk, uint32_t flags);
 
 /* Device time of the last batch's crypto kernel (ms, from HIP events on the
  * batch stream), for the roofline accounting in bench.py. */

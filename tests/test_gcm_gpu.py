@@ -305,3 +305,37 @@ def test_full_size_roundtrip_1m_x_1500(drv):
         assert e == 0
         assert dec[16:rec - 16] == plain[o + 16:o + rec - 16].cpu().numpy().tobytes()
     drv.freesession(sids[0])
+
+
+@pytest.mark.parametrize("chunk", [0, 97, 1000])
+def test_host_pipeline_vs_oracle(drv, chunk):
+    """espgpu_decrypt_host: pinned host records -> chunked H2D/kernel/D2H on
+    three streams -> pinned host plaintext; same results as the oracle."""
+    from espgpu.batch import decrypt_host
+    rng = np.random.default_rng(500 + chunk)
+    sas = [GcmSA(rng, 16), GcmSA(rng, 32, esn=True)]
+    sids = _sessions(drv, sas)
+    n = 2500
+    sa_idx = rng.integers(0, 2, n)
+    cts = rng.choice([4, 16, 204, 1448, 8948], n)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts,
+                                         esn_hi=rng.integers(0, 2**32, n, dtype=np.uint32))
+    bad = ct.copy()
+    flip = rng.random(n) < 0.05
+    for i in np.nonzero(flip)[0]:
+        bad[int(descs["off4"][i]) * 4 + int(descs["len"][i]) - 3] ^= 0x01
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    h_arena = torch.from_numpy(bad.copy()).pin_memory()
+    h_desc = torch.from_numpy(np.ascontiguousarray(d).view(np.uint8).copy()).pin_memory()
+    h_out = torch.zeros(len(bad), dtype=torch.uint8).pin_memory()
+    h_st = torch.full((n,), 0xEE, dtype=torch.uint8).pin_memory()
+    decrypt_host(drv, h_arena, h_desc, n, h_st, h_out, chunk=chunk)
+    st = h_st.numpy()
+    assert (st == ref_st).all(), np.nonzero(st != ref_st)[0][:10]
+    m = payload_mask(descs[st == 0], len(bad))
+    assert (h_out.numpy()[m] == ref_out[m]).all()
+    assert (h_out.numpy()[m] == plain[m]).all()
+    for s in sids:
+        drv.freesession(s)
