@@ -486,12 +486,19 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
 
   const bool implicit = (p.chunks == nullptr);
   const uint32_t nch = implicit ? (p.n + kChunkRecs - 1) / kChunkRecs : *p.nchunks;
-  const uint32_t c0 = (uint32_t)(((uint64_t)blockIdx.x * nch) / gridDim.x);
-  const uint32_t c1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * nch) / gridDim.x);
   uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
   const int wave = tid >> 6;
-
-  for (uint32_t c = c0; c < c1; ++c) {
+  // Dynamic chunk queue: chunk costs differ by up to ~300x (64-B vs 9000-B
+  // records) and the planner emits the largest first, so grabbing tickets
+  // balances the chip where a static split would leave most CUs idle.
+  // s_ticket is double-buffered by iteration parity: slot it&1 is rewritten
+  // only at it+2, after every thread passed iteration it+1's barrier.
+  __shared__ uint32_t s_ticket[2];
+  for (uint32_t it = 0;; ++it) {
+    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
+    __syncthreads();
+    const uint32_t c = s_ticket[it & 1];
+    if (c >= nch) break;
     uint32_t sa, start, count;
     if (implicit) {
       start = c * kChunkRecs;
@@ -536,6 +543,12 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
       do_group<MODE, FUSE>(p, lds, di, have, sa, flags, mlen, (int)nr,
                            (rkptr)(const void *)(p.sas[sa].rk));
     }
+  }
+  // Every workgroup leaves the loop after drawing exactly one ticket >= nch,
+  // so once all have retired no ticket is drawn again: reset for the next launch.
+  if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
+    atomicExch(&p.queue[0], 0u);
+    atomicExch(&p.queue[1], 0u);
   }
 }
 

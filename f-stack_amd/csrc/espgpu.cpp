@@ -82,6 +82,7 @@ struct espgpu_ctx {
   uint8_t *d_gtab = nullptr;
   uint2 *d_tpair = nullptr, *d_dpair = nullptr;
   uint8_t *d_isbox = nullptr;
+  uint32_t *d_queue = nullptr;   // GCM work-queue ticket + retire counters (self-resetting)
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
   int n_eta = 0;
@@ -202,6 +203,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   p.tpair = c->d_tpair;
   p.status = d_status;
   p.nsas = nsas;
+  p.queue = c->d_queue;
   if (!(flags & ESPGPU_BATCH_GROUPED)) {
     int e = ensure_plan(c, n);
     if (e) return e;
@@ -276,11 +278,13 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
         hipMalloc(&c->d_gtab, (size_t)cfg.max_sessions * kGhTableBytes) != hipSuccess ||
         hipMalloc(&c->d_tpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_dpair, 256 * sizeof(uint2)) != hipSuccess ||
-        hipMalloc(&c->d_isbox, 256) != hipSuccess) {
+        hipMalloc(&c->d_isbox, 256) != hipSuccess ||
+        hipMalloc(&c->d_queue, 16) != hipSuccess) {
       rc = fail(c, ENOMEM, "device SA table allocation failed");
       break;
     }
     hipMemset(c->d_sas, 0, (size_t)cfg.max_sessions * sizeof(DevSA));
+    hipMemset(c->d_queue, 0, 16);
     const hc::Tables &t = hc::tables();
     uint2 tp[256], dp[256];
     for (int x = 0; x < 256; ++x) {
@@ -315,6 +319,7 @@ void espgpu_fini(espgpu_ctx *c) {
     if (c->e2e_k[k]) hipEventDestroy(c->e2e_k[k]);
   }
   hipFree(c->d_sas); hipFree(c->d_gtab); hipFree(c->d_tpair); hipFree(c->d_dpair); hipFree(c->d_isbox);
+  hipFree(c->d_queue);
   hipFree(c->d_work); hipFree(c->d_order); hipFree(c->d_chunks); hipFree(c->d_nchunks);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);

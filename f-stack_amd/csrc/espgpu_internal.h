@@ -58,6 +58,10 @@ struct GcmParams {
   const uint2 *tpair;             // 256 x (Te0[x], Te1[x])
   uint8_t *status;
   uint32_t nsas;
+  // Work queue: [0] next chunk ticket, [1] retired workgroups.  Zero before a
+  // launch; the last workgroup to retire resets both, so no per-launch memset.
+  // Launches sharing a ctx must be stream-ordered (as the planner workspace).
+  uint32_t *queue;
 };
 
 struct EtaParams {

@@ -8,7 +8,7 @@
 //                and chunk offsets; writes the chunk list and its length
 //   plan_scatter per-workgroup LDS ranks + one global range reservation per
 //                non-empty key -> order[] (a permutation of descriptor ids)
-// Keys: [0, 4*nsas) = GCM records (class-major), 4*nsas = records of ETA
+// Keys: [0, 4*nsas) = GCM records (class-major, largest class first), 4*nsas = records of ETA
 // sessions (not chunked: the ETA kernel walks descriptors directly),
 // 4*nsas+1 = records with no valid session (chunked with sa = ~0 so the GCM
 // kernel marks them EINVAL).  Cost: two passes over the 16-byte descriptors.
@@ -39,7 +39,9 @@ __device__ __forceinline__ uint32_t key_of(const espgpu_desc &d, const DevSA *sa
   const uint32_t mode = sas[sa].mode;
   if (mode == ESPGPU_CSP_MODE_ETA) return 4 * nsas;
   if (mode != ESPGPU_CSP_MODE_AEAD) return 4 * nsas + 1;
-  return size_class(d.len) * nsas + sa;
+  // largest class first: with the GCM kernel's dynamic chunk queue this is
+  // longest-processing-time-first scheduling
+  return (3u - size_class(d.len)) * nsas + sa;
 }
 
 __global__ __launch_bounds__(PWG) void plan_count(const espgpu_desc *desc, uint32_t n,
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t 
     gcur[k] = roff;
     if (is_chunked(k)) {
       const uint32_t sa = (k == 4 * nsas + 1) ? 0xffffffffu : k % nsas;
-      const uint32_t cls = (k == 4 * nsas + 1) ? 0u : k / nsas;
+      const uint32_t cls = (k == 4 * nsas + 1) ? 0u : 3u - k / nsas;
       for (uint32_t j = 0; j * kChunkRecs < cnt; ++j, ++coff) {
         if (coff < max_chunks)
           chunks[coff] = Chunk{sa, roff + j * kChunkRecs, min((uint32_t)kChunkRecs, cnt - j * kChunkRecs), cls};
