@@ -151,7 +151,11 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
 // S-box copy in global memory for the experimental L1-gather last round
 // (variant bit 2): spreads lookups over the vector-memory path as well as LDS.
 __device__ uint8_t g_sbox[256];
-__device__ uint32_t g_opts;   // bit0: L1-gather last round
+// Runtime options (wave-uniform scalar loads): bit0 L1-gather last round;
+// bits 1-2 are measurement knobs that break results on purpose (bit1 skips
+// the GHASH multiply, bit2 the AES rounds) to split the kernel's time.
+__device__ uint32_t g_opts;
+__device__ __forceinline__ uint32_t gopts() { return *(const __attribute__((address_space(4))) uint32_t *)(const void *)&g_opts; }
 
 // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
 // words directly; the last round key is stored byte-swapped.
@@ -187,12 +191,13 @@ __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s
   // nr and rk are wave-uniform (one session per chunk): one loop body serves
   // AES-128/192/256, and the round keys come in through scalar loads (SGPRs),
   // not LDS, which is the bottleneck resource.
+  if (gopts() & 4) return make_uint4(s0, s1, s2, s3);
 #pragma unroll 1
   for (int r = r0; r < nr; ++r) {
     aes_round(s0, s1, s2, s3, ldk4(rk + 4 * r), lds, slot);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (*(rkptr)(const void *)&g_opts & 1)
+  if (gopts() & 1)
     return aes_last<true>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
   return aes_last<false>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
 }
@@ -394,6 +399,11 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   for (int m = 0; m < Mw; ++m) {
     const int i = S * m + l - pad;
     const uint32_t ctr = i >= 0 ? (uint32_t)(i + 1) : 1u;     // J0 for block 0, c+2 for CT c
+    // Issue this step's ciphertext load before the AES/GHASH work so its HBM
+    // latency hides under ~500 instructions instead of stalling the store.
+    const bool has_ct = valid && i >= 1 && i <= nct;
+    uint4 C = make_uint4(0, 0, 0, 0);
+    if (has_ct) C = ld16(rec + 16 + 16 * (i - 1));
     if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
     uint4 ks = make_uint4(0, 0, 0, 0);
     if (MODE != 2 && FUSE) {
@@ -403,17 +413,16 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
                    : ctr_ghash_step<false>(cc, ctr, rk3, nr, Yn, rk, lds, slot);
       if (m < M) Y = Yn;
     } else {
-      if (m > 0) {
+      if (m > 0 && !(gopts() & 2)) {
         const uint4 Yn = gf_mul(Y, LDS_GT + 7 * 8192, lds);
         if (m < M) Y = Yn;
       }
       if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
     }
     uint4 B = make_uint4(0, 0, 0, 0);
-    if (valid && i >= 1 && i <= nct) {
+    if (has_ct) {
       const int c = i - 1;
       const int rem = ct_len - 16 * c;
-      const uint4 C = ld16(rec + 16 + 16 * c);
       if (MODE == 1) {
         const uint4 o = xor4(C, ks);
         st_partial(orec + 16 + 16 * c, o, rem);
@@ -573,7 +582,7 @@ int gcm_set_sbox(const uint8_t *sbox256) {
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   static int cur_opts = -1;
-  const uint32_t opts = (variant >> 2) & 1;
+  const uint32_t opts = (uint32_t)variant >> 2;
   if ((int)opts != cur_opts) {
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_opts), &opts, 4, 0, hipMemcpyHostToDevice, st);
     hipStreamSynchronize(st);

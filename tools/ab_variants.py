@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--pkt", type=int, default=1500)
+    ap.add_argument("--no-check", action="store_true", help="for measurement-only variants")
     args = ap.parse_args()
     import torch
     from espgpu.batch import decrypt_batch, encrypt_batch
@@ -49,7 +50,7 @@ def main():
                 drv.lib.espgpu_set_tuning(drv.ctx, b"grid", g)
                 decrypt_batch(drv, arena, desc, n, st, out=out, grouped=True)
                 torch.cuda.synchronize()
-                assert int((st != 0).sum()) == 0, (v, g)
+                assert args.no_check or int((st != 0).sum()) == 0, (v, g)
                 e0.record()
                 for _ in range(args.steps):
                     decrypt_batch(drv, arena, desc, n, st, out=out, grouped=True)
