@@ -253,12 +253,29 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   }
   __syncthreads();
 
-  const uint32_t waves = gridDim.x * (WG / 64);
-  const uint32_t wave = blockIdx.x * (WG / 64) + (tid >> 6);
-  for (uint32_t base = wave * 64; base < p.n; base += waves * 64) {
+  // Work units are one wave's worth of records: a 64-record ETA chunk of one
+  // session from the planner, or (implicit) 64 consecutive descriptors.
+  // Waves draw units from a queue; the last wave to retire resets it.
+  const bool implicit = p.chunks == nullptr;
+  const uint32_t u0 = implicit ? 0u : p.nchunks[0];
+  const uint32_t u1 = implicit ? (p.n + 63) / 64 : p.nchunks[1];
+  for (;;) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&p.queue[0], 1u);
+    const uint32_t u = u0 + __builtin_amdgcn_readfirstlane(t);
+    if (u >= u1) break;
+    uint32_t di = 0;
+    bool have;
+    if (implicit) {
+      di = u * 64 + lane;
+      have = di < p.n;
+    } else {
+      const Chunk ch = p.chunks[u];
+      have = (uint32_t)lane < ch.count;
+      if (have) di = p.order[ch.start + lane];
+    }
     // ---- lane = record: descriptor, HMAC (verify or compute) ----
-    const uint32_t di = base + lane;
-    bool have = di < p.n, valid = false, ok = false;
+    bool valid = false, ok = false;
     uint32_t off = 0, len = 0, sa = 0, plen = 0;
     if (have) {
       const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
@@ -309,33 +326,62 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
     }
     if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 
-    // ---- decrypt: the wave walks its records; lanes split each record's blocks ----
-    const bool run_me = have && valid && (MODE == 0 || ok);
-    uint64_t todo = __ballot(run_me);
+    // ---- decrypt: all of the wave's blocks of one session as one flat list ----
+    // Records to decrypt (one session at a time, so the round keys stay
+    // wave-uniform in SGPRs: one pass for planner chunks) are concatenated;
+    // every lane takes one block per pass, last pass first.  Within a pass all
+    // lanes load C_i and C_{i-1} before any lane stores, and a pass only
+    // overwrites blocks no later (lower) pass reads: in-place decryption is
+    // safe without holding records in registers.
+    bool run = have && valid && (MODE == 0 || ok);
+    uint64_t todo = __ballot(run);
     while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint32_t roff = __shfl(off, j), rplen = __shfl(plen, j), rsa = __shfl(sa, j);
-      const DevSA *s = p.sas + __builtin_amdgcn_readfirstlane(rsa);
+      const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
+      const bool mine = run && sa == sau;
+      todo &= ~__ballot(mine);
+      run = run && !mine;
+      const uint32_t nb = mine ? plen / 16 : 0;
+      uint32_t incl = nb;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const uint32_t start = incl - nb;
+      const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
+      const DevSA *s = p.sas + sau;
       const int nr = (int)s->nr;
       const kptr dk = kp(s->dk);
-      const uint8_t *rec = p.arena + __builtin_amdgcn_readfirstlane(roff);
-      uint8_t *orec = (MODE == 0 ? p.out : p.arena) + __builtin_amdgcn_readfirstlane(roff);
-      const uint32_t nblk = __builtin_amdgcn_readfirstlane(rplen) / 16;
-      // Passes of 64 consecutive blocks, last pass first: within a pass every
-      // lane loads C_i and C_{i-1} before any lane stores, and a pass only
-      // overwrites blocks that no later (lower) pass reads, so in-place
-      // decryption is safe without holding the record in registers.
-      for (int pb = (int)((nblk - 1) & ~63u); pb >= 0; pb -= 64) {
-        const uint32_t i = (uint32_t)pb + lane;
-        if (i < nblk) {
+      uint8_t *const obase = MODE == 0 ? p.out : p.arena;
+      for (int base = total - 64; base > -64; base -= 64) {
+        const int f = base + lane;
+        // the record holding flat block f: the last lane whose start <= f
+        int j = 0;
+        uint32_t sj = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+          const uint32_t sc = __shfl(start, j + step);
+          if ((int)sc <= f) {
+            j += step;
+            sj = sc;
+          }
+        }
+        const uint32_t ro = __shfl(off, j);
+        if (f >= 0) {
+          const uint32_t i = (uint32_t)f - sj;
+          const uint8_t *rec = p.arena + ro;
           const uint4 c = ld16(rec + 24 + 16 * i);
           const uint4 prev = ld16(rec + 8 + 16 * i);         // C_{i-1}, or the IV for i = 0
-          const uint4 pt = xor4(aes_dec(c, dk, nr, lds, slot), prev);
-          st16(orec + 24 + 16 * i, pt);
+          st16(obase + ro + 24 + 16 * i, xor4(aes_dec(c, dk, nr, lds, slot), prev));
         }
       }
     }
+  }
+  // Every wave leaves the loop after drawing one ticket past the end, so once
+  // all have retired no ticket is drawn again: reset for the next launch.
+  if (lane == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x * (WG / 64) - 1) {
+    atomicExch(&p.queue[0], 0u);
+    atomicExch(&p.queue[1], 0u);
   }
 }
 

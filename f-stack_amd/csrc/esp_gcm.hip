@@ -40,8 +40,10 @@ namespace espgpu {
 namespace {
 
 constexpr uint32_t LDS_TP = 0;          // 256 entries x 32 lane slots x 8 B
-constexpr uint32_t LDS_GT = 65536;      // 8 powers x 32 positions x 16 x 16 B
-constexpr uint32_t LDS_BYTES = 131072;
+constexpr uint32_t LDS_GT = 65536;      // GHASH tables: H^1..H^8, H^16 (8 KiB each)
+constexpr uint32_t LDS_BYTES = LDS_GT + kGhTableBytes;
+constexpr uint32_t PW8 = LDS_GT + 7 * kGhPowerBytes;    // H^8
+constexpr uint32_t PW16 = LDS_GT + 8 * kGhPowerBytes;   // H^16
 constexpr int S = 8;                    // lanes per record
 
 // Round keys are read through the constant address space: uniform loads from
@@ -55,14 +57,6 @@ struct __attribute__((aligned(4))) U4 {
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-// Same operation as an opaque asm: LLVM may not reassociate across it, which
-// keeps each GHASH lookup group's XOR folding next to its loads (otherwise the
-// XOR chain is re-associated to the end and every lookup result stays live).
-__device__ __forceinline__ uint32_t xor3_pin(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
 }
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
   return __builtin_amdgcn_perm(hi, lo, sel);
@@ -148,38 +142,26 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
   s3 = xor3(a3, b3, ror16(xor3(c3, d3, k.w)));
 }
 
-// S-box copy in global memory for the experimental L1-gather last round
-// (variant bit 2): spreads lookups over the vector-memory path as well as LDS.
-__device__ uint8_t g_sbox[256];
-// Runtime options (wave-uniform scalar loads): bit0 L1-gather last round;
-// bits 1-2 are measurement knobs that break results on purpose (bit1 skips
-// the GHASH multiply, bit2 the AES rounds) to split the kernel's time.
+// Runtime options (wave-uniform scalar loads).  Measurement knobs that break
+// results on purpose, to split the kernel's time: bit1 skips the GHASH
+// multiplies of the main loop, bit2 the AES rounds after round 2.
 __device__ uint32_t g_opts;
 __device__ __forceinline__ uint32_t gopts() { return *(const __attribute__((address_space(4))) uint32_t *)(const void *)&g_opts; }
 
 // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
 // words directly; the last round key is stored byte-swapped.
-template <bool LASTG>
 __device__ __forceinline__ uint4 aes_last(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint4 k,
                                           const uint8_t *lds, uint32_t slot) {
-  uint32_t a, b, c, d, o[4];
-  uint32_t ss[4] = {s0, s1, s2, s3};
-  uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+  uint32_t o[4];
+  const uint32_t ss[4] = {s0, s1, s2, s3};
+  const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
 #pragma unroll
   for (int col = 0; col < 4; ++col) {
-    if (LASTG) {
-      a = g_sbox[ss[col] >> 24];
-      b = g_sbox[(ss[(col + 1) & 3] >> 16) & 0xff];
-      c = g_sbox[(ss[(col + 2) & 3] >> 8) & 0xff];
-      d = g_sbox[ss[(col + 3) & 3] & 0xff];
-      o[col] = (a | (b << 8) | (c << 16) | (d << 24)) ^ kk[col];
-    } else {
-      a = te0(lds, tpa(ss[col], slot, 3));
-      b = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
-      c = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
-      d = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
-      o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
-    }
+    const uint32_t a = te0(lds, tpa(ss[col], slot, 3));
+    const uint32_t b = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
+    const uint32_t c = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
+    const uint32_t d = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
+    o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
@@ -197,9 +179,7 @@ __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s
     aes_round(s0, s1, s2, s3, ldk4(rk + 4 * r), lds, slot);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (gopts() & 1)
-    return aes_last<true>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
-  return aes_last<false>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
+  return aes_last(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
 }
 
 // ---- counter-mode caching of rounds 1-2 ------------------------------------
@@ -253,6 +233,36 @@ __device__ __forceinline__ uint4 aes_ctr(const CtrCache &cc, uint32_t ctr, uint3
   return aes_rounds(v0, v1, v2, v3, 3, nr, rk, lds, slot);
 }
 
+// Two counter blocks (both covered by the cache) interleaved round by round:
+// each round issues 32 independent LDS lookups before the wave waits, halving
+// the dependent LDS round trips per block.
+__device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32_t cb, uint32_t rk3,
+                                         int nr, rkptr rk, const uint8_t *lds, uint32_t slot,
+                                         uint4 &ka, uint4 &kb) {
+  const uint32_t ta = cc.K0 ^ ror16(te1(lds, tpa(ca ^ rk3, slot, 0)));
+  const uint32_t tb = cc.K0 ^ ror16(te1(lds, tpa(cb ^ rk3, slot, 0)));
+  uint32_t a0 = cc.L0 ^ te0(lds, tpa(ta, slot, 3)), b0 = cc.L0 ^ te0(lds, tpa(tb, slot, 3));
+  uint32_t a1 = cc.L1 ^ ror16(te1(lds, tpa(ta, slot, 0))), b1 = cc.L1 ^ ror16(te1(lds, tpa(tb, slot, 0)));
+  uint32_t a2 = cc.L2 ^ ror16(te0(lds, tpa(ta, slot, 1))), b2 = cc.L2 ^ ror16(te0(lds, tpa(tb, slot, 1)));
+  uint32_t a3 = cc.L3 ^ te1(lds, tpa(ta, slot, 2)), b3 = cc.L3 ^ te1(lds, tpa(tb, slot, 2));
+  if (gopts() & 4) {
+    ka = make_uint4(a0, a1, a2, a3);
+    kb = make_uint4(b0, b1, b2, b3);
+    return;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+  for (int r = 3; r < nr; ++r) {
+    const uint4 k = ldk4(rk + 4 * r);
+    aes_round(a0, a1, a2, a3, k, lds, slot);
+    aes_round(b0, b1, b2, b3, k, lds, slot);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const uint4 kl = ldk4(rk + 4 * nr);
+  ka = aes_last(a0, a1, a2, a3, kl, lds, slot);
+  kb = aes_last(b0, b1, b2, b3, kl, lds, slot);
+}
+
 // ---- GHASH multiply by a fixed power (gf128_mul, gfmult.c:219-229) ----------
 // pb = LDS byte address of the power's 8 KiB table (low byte 0, < 2^24).
 // Nibble position j = 8k + 2q (+1 for the high nibble) of word k, byte q.
@@ -287,52 +297,44 @@ __device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds
   return make_uint4(r0, r1, r2, r3);
 }
 
-// 8 lookups of one 32-bit word (nibble positions 8k..8k+7), accumulated into r*.
-__device__ __forceinline__ void gf_group(uint32_t w, uint32_t pb, uint32_t &r0, uint32_t &r1,
-                                         uint32_t &r2, uint32_t &r3, const uint8_t *lds) {
-  const uint32_t hi = w & 0xF0F0F0F0u, lo = (w << 4) & 0xF0F0F0F0u;
+// Two independent products x * P and y * Q in one rolled word loop: 4 table
+// rows in flight per lookup group instead of 2.
+__device__ __forceinline__ void gf_mul2(uint4 x, uint32_t px, uint4 y, uint32_t py,
+                                        const uint8_t *lds, uint4 &rx, uint4 &ry) {
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+  uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
+  uint32_t v = y.x, v1 = y.y, v2 = y.z, v3 = y.w;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t hw = w & 0xF0F0F0F0u, lw = (w << 4) & 0xF0F0F0F0u;
+    const uint32_t hv = v & 0xF0F0F0F0u, lv = (v << 4) & 0xF0F0F0F0u;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t sel = 0x0c060500u | (uint32_t)q;
-    const uint4 e = *reinterpret_cast<const uint4 *>(lds + perm(pb, lo, sel) + (2 * q) * 256);
-    const uint4 f = *reinterpret_cast<const uint4 *>(lds + perm(pb, hi, sel) + (2 * q + 1) * 256);
-    r0 = xor3_pin(r0, e.x, f.x);
-    r1 = xor3_pin(r1, e.y, f.y);
-    r2 = xor3_pin(r2, e.z, f.z);
-    r3 = xor3_pin(r3, e.w, f.w);
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t sel = 0x0c060500u | (uint32_t)q;
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + perm(px, lw, sel) + (2 * q) * 256);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + perm(px, hw, sel) + (2 * q + 1) * 256);
+      const uint4 g = *reinterpret_cast<const uint4 *>(lds + perm(py, lv, sel) + (2 * q) * 256);
+      const uint4 h = *reinterpret_cast<const uint4 *>(lds + perm(py, hv, sel) + (2 * q + 1) * 256);
+      a0 = xor3(a0, e.x, f.x);
+      a1 = xor3(a1, e.y, f.y);
+      a2 = xor3(a2, e.z, f.z);
+      a3 = xor3(a3, e.w, f.w);
+      b0 = xor3(b0, g.x, h.x);
+      b1 = xor3(b1, g.y, h.y);
+      b2 = xor3(b2, g.z, h.z);
+      b3 = xor3(b3, g.w, h.w);
+    }
+    w = w1;
+    w1 = w2;
+    w2 = w3;
+    v = v1;
+    v1 = v2;
+    v2 = v3;
+    px += 8 * 256;
+    py += 8 * 256;
   }
-}
-
-// One pipeline step of a lane: E_K(nonce||ctr) and, when GH, Y <- Y * H^8.
-// The two are independent, so each GHASH word group is issued in the same
-// LDS batch as an AES round: the wave waits on 9 dependent LDS round trips per
-// step instead of 13, and the LDS sees 16-24 lookups per batch.
-template <bool GH>
-__device__ __forceinline__ uint4 ctr_ghash_step(const CtrCache &cc, uint32_t ctr, uint32_t rk3, int nr,
-                                                uint4 &Y, rkptr rk, const uint8_t *lds,
-                                                uint32_t slot) {
-  const uint32_t pb = LDS_GT + 7 * 8192;                  // H^8
-  uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0;
-  // rounds 1-2 from the counter cache (1 + 4 lookups) || GHASH word 0
-  if (GH) gf_group(Y.x, pb, g0, g1, g2, g3, lds);
-  const uint32_t t0 = cc.K0 ^ ror16(te1(lds, tpa(ctr ^ rk3, slot, 0)));
-  uint32_t s0 = cc.L0 ^ te0(lds, tpa(t0, slot, 3));
-  uint32_t s1 = cc.L1 ^ ror16(te1(lds, tpa(t0, slot, 0)));
-  uint32_t s2 = cc.L2 ^ ror16(te0(lds, tpa(t0, slot, 1)));
-  uint32_t s3 = cc.L3 ^ te1(lds, tpa(t0, slot, 2));
-  __builtin_amdgcn_sched_barrier(0);
-  // rounds 3-5 || GHASH words 1-3
-  if (GH) gf_group(Y.y, pb + 2048, g0, g1, g2, g3, lds);
-  aes_round(s0, s1, s2, s3, ldk4(rk + 12), lds, slot);
-  __builtin_amdgcn_sched_barrier(0);
-  if (GH) gf_group(Y.z, pb + 4096, g0, g1, g2, g3, lds);
-  aes_round(s0, s1, s2, s3, ldk4(rk + 16), lds, slot);
-  __builtin_amdgcn_sched_barrier(0);
-  if (GH) gf_group(Y.w, pb + 6144, g0, g1, g2, g3, lds);
-  aes_round(s0, s1, s2, s3, ldk4(rk + 20), lds, slot);
-  __builtin_amdgcn_sched_barrier(0);
-  if (GH) Y = make_uint4(g0, g1, g2, g3);
-  return aes_rounds(s0, s1, s2, s3, 6, nr, rk, lds, slot);
+  rx = make_uint4(a0, a1, a2, a3);
+  ry = make_uint4(b0, b1, b2, b3);
 }
 
 __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
@@ -349,7 +351,9 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
-template <int MODE, bool FUSE>
+// PAIR: steps m, m+1 of a lane run together (2 independent AES blocks, and
+// Y <- Y*H^16 ^ B_m*H^8 ^ B_m+1 as 2 independent GHASH products).
+template <int MODE, bool PAIR>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di,
                                                    bool have, uint32_t sa, uint32_t sa_flags,
                                                    uint32_t mlen, int nr, rkptr rk) {
@@ -395,52 +399,79 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   CtrCache cc;
   cc.hi = -1;                                               // built on first use
 
-  uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
-  for (int m = 0; m < Mw; ++m) {
-    const int i = S * m + l - pad;
-    const uint32_t ctr = i >= 0 ? (uint32_t)(i + 1) : 1u;     // J0 for block 0, c+2 for CT c
-    // Issue this step's ciphertext load before the AES/GHASH work so its HBM
-    // latency hides under ~500 instructions instead of stalling the store.
-    const bool has_ct = valid && i >= 1 && i <= nct;
-    uint4 C = make_uint4(0, 0, 0, 0);
-    if (has_ct) C = ld16(rec + 16 + 16 * (i - 1));
-    if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
-    uint4 ks = make_uint4(0, 0, 0, 0);
-    if (MODE != 2 && FUSE) {
-      // keystream || Y * H^8 (a record shorter than the wave's longest keeps its hash)
-      uint4 Yn = Y;
-      ks = (m > 0) ? ctr_ghash_step<true>(cc, ctr, rk3, nr, Yn, rk, lds, slot)
-                   : ctr_ghash_step<false>(cc, ctr, rk3, nr, Yn, rk, lds, slot);
-      if (m < M) Y = Yn;
-    } else {
-      if (m > 0 && !(gopts() & 2)) {
-        const uint4 Yn = gf_mul(Y, LDS_GT + 7 * 8192, lds);
-        if (m < M) Y = Yn;
-      }
-      if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
-    }
-    uint4 B = make_uint4(0, 0, 0, 0);
+  // GHASH input block of GHASH index i (>= 1) given its ciphertext C and
+  // keystream ks; stores the output block (MODE 0: plaintext, MODE 1: CT).
+  auto block_in = [&](int i, bool has_ct, uint4 C, uint4 ks) -> uint4 {
     if (has_ct) {
       const int c = i - 1;
       const int rem = ct_len - 16 * c;
       if (MODE == 1) {
         const uint4 o = xor4(C, ks);
         st_partial(orec + 16 + 16 * c, o, rem);
-        B = mask_block(o, rem);
-      } else {
-        B = mask_block(C, rem);
-        if (MODE == 0) st_partial(orec + 16 + 16 * c, xor4(C, ks), rem);
+        return mask_block(o, rem);
       }
-    } else if (valid && i == 0) {
+      if (MODE == 0) st_partial(orec + 16 + 16 * c, xor4(C, ks), rem);
+      return mask_block(C, rem);
+    }
+    if (valid && i == N - 1)                                     // length block
+      return make_uint4(0, bswap32(sep ? 96u : 64u), 0, bswap32((uint32_t)ct_len * 8));
+    return make_uint4(0, 0, 0, 0);
+  };
+
+  uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
+  int m = 0;
+  while (m < Mw) {
+    const int i = S * m + l - pad;
+    if (PAIR && m > 0 && m + 1 < Mw) {
+      // i >= 1 here; the pair needs the counter cache valid for both blocks
+      const uint32_t ca = (uint32_t)i + 1, cb = ca + S;
+      if (__all((int)(ca >> 8) == cc.hi && (int)(cb >> 8) == cc.hi)) {
+        const int ib = i + S;
+        const bool hca = valid && i <= nct, hcb = valid && ib <= nct;
+        uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+        if (hca) Ca = ld16(rec + 16 * i);
+        if (hcb) Cb = ld16(rec + 16 * ib);
+        uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
+        if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+        const uint4 Ba = block_in(i, hca, Ca, ka);
+        const uint4 Bb = block_in(ib, hcb, Cb, kb);
+        if (!(gopts() & 2)) {
+          // M >= m+2: Y = Y*H^16 ^ Ba*H^8 ^ Bb;  M == m+1: Y = Y*H^8 ^ Ba
+          const bool two = M >= m + 2;
+          uint4 P, Q;
+          gf_mul2(Y, two ? PW16 : PW8, Ba, PW8, lds, P, Q);
+          if (two) Y = xor4(xor4(P, Q), Bb);
+          else if (M == m + 1) Y = xor4(P, Ba);
+        }
+        m += 2;
+        continue;
+      }
+    }
+    const uint32_t ctr = i >= 0 ? (uint32_t)(i + 1) : 1u;     // J0 for block 0, c+2 for CT c
+    // Issue this step's ciphertext load before the AES/GHASH work so its HBM
+    // latency hides under the round computation.
+    const bool has_ct = valid && i >= 1 && i <= nct;
+    uint4 C = make_uint4(0, 0, 0, 0);
+    if (has_ct) C = ld16(rec + 16 * i);
+    if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
+    uint4 ks = make_uint4(0, 0, 0, 0);
+    if (m > 0 && !(gopts() & 2)) {
+      const uint4 Yn = gf_mul(Y, PW8, lds);
+      if (m < M) Y = Yn;
+    }
+    if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
+    uint4 B;
+    if (valid && i == 0) {
       B = sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0);     // AAD block
       EJ0 = ks;
-    } else if (valid && i == N - 1) {
-      B = make_uint4(0, bswap32(sep ? 96u : 64u), 0, bswap32((uint32_t)ct_len * 8));   // len block
+    } else {
+      B = block_in(i, has_ct, C, ks);
     }
     Y = xor4(Y, B);
+    ++m;
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
-  uint4 Z = gf_mul(Y, LDS_GT + (uint32_t)(7 - l) * 8192, lds);
+  uint4 Z = gf_mul(Y, LDS_GT + (uint32_t)(7 - l) * kGhPowerBytes, lds);
   Z = xor4(Z, shfl_xor4(Z, 1));
   Z = xor4(Z, shfl_xor4(Z, 2));
   Z = xor4(Z, shfl_xor4(Z, 4));
@@ -480,7 +511,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
-template <int MODE, int WG, bool FUSE>
+template <int MODE, int WG, bool PAIR>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -549,7 +580,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         if (mode == 0 && have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
         continue;
       }
-      do_group<MODE, FUSE>(p, lds, di, have, sa, flags, mlen, (int)nr,
+      do_group<MODE, PAIR>(p, lds, di, have, sa, flags, mlen, (int)nr,
                            (rkptr)(const void *)(p.sas[sa].rk));
     }
   }
@@ -564,7 +595,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
 }  // namespace
 
 // variant: bit0 = 512-thread workgroups (2 waves/SIMD, 256 VGPRs) instead of
-// 1024 (4 waves/SIMD, 128 VGPRs); bit1 = fuse GHASH word groups into AES rounds.
+// 1024 (4 waves/SIMD, 128 VGPRs); bit1 = PAIR (two steps per lane at once).
 template <int MODE>
 static void launch_mode(const GcmParams &p, int variant, int grid, hipStream_t st) {
   switch (variant & 3) {
@@ -573,10 +604,6 @@ static void launch_mode(const GcmParams &p, int variant, int grid, hipStream_t s
     case 2: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true>), dim3(grid), dim3(1024), 0, st, p); break;
     default: hipLaunchKernelGGL((gcm_kernel<MODE, 512, true>), dim3(grid), dim3(512), 0, st, p); break;
   }
-}
-
-int gcm_set_sbox(const uint8_t *sbox256) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_sbox), sbox256, 256) == hipSuccess ? 0 : -1;
 }
 
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream) {

@@ -82,7 +82,7 @@ struct espgpu_ctx {
   uint8_t *d_gtab = nullptr;
   uint2 *d_tpair = nullptr, *d_dpair = nullptr;
   uint8_t *d_isbox = nullptr;
-  uint32_t *d_queue = nullptr;   // GCM work-queue ticket + retire counters (self-resetting)
+  uint32_t *d_queue = nullptr;   // work queues: [0..1] GCM, [2..3] ETA (ticket, retired; self-resetting)
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
   int n_eta = 0;
@@ -127,16 +127,17 @@ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
 uint32_t ror16(uint32_t v) { return (v >> 16) | (v << 16); }
 
 int ensure_plan(espgpu_ctx *c, uint32_t n) {
-  const uint32_t nsas = (uint32_t)c->sessions.size();
-  const uint32_t need_chunks = n / kChunkRecs + 4 * nsas + 8;
+  const uint32_t need_chunks = plan_max_chunks(n, c->cfg.max_sessions);
   if (n <= c->plan_cap && need_chunks <= c->max_chunks) return 0;
   hipFree(c->d_work);
   hipFree(c->d_order);
   hipFree(c->d_chunks);
   hipFree(c->d_nchunks);
   c->plan_cap = std::max(n, 1024u);
-  c->max_chunks = c->plan_cap / kChunkRecs + 4 * nsas + 8;
-  HIPCHK(c, hipMalloc(&c->d_work, plan_workspace_words(nsas) * 4));
+  c->max_chunks = plan_max_chunks(c->plan_cap, c->cfg.max_sessions);
+  // key histograms sized for the SA table's capacity: sessions created after
+  // this allocation must not outgrow it
+  HIPCHK(c, hipMalloc(&c->d_work, plan_workspace_words(c->cfg.max_sessions) * 4));
   HIPCHK(c, hipMalloc(&c->d_order, (size_t)c->plan_cap * 4));
   HIPCHK(c, hipMalloc(&c->d_chunks, (size_t)c->max_chunks * sizeof(Chunk)));
   HIPCHK(c, hipMalloc(&c->d_nchunks, 16));
@@ -221,6 +222,10 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.arena = d_arena;
     q.out = p.out;
     q.desc = d_desc;
+    q.order = p.order;
+    q.chunks = p.chunks;
+    q.nchunks = p.nchunks;
+    q.queue = c->d_queue + 2;
     q.n = n;
     q.sas = c->d_sas;
     q.tpair = c->d_tpair;
@@ -294,7 +299,6 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     hipMemcpy(c->d_tpair, tp, sizeof tp, hipMemcpyHostToDevice);
     hipMemcpy(c->d_dpair, dp, sizeof dp, hipMemcpyHostToDevice);
     hipMemcpy(c->d_isbox, t.isbox, 256, hipMemcpyHostToDevice);
-    gcm_set_sbox(t.sbox);
     c->slots.resize(cfg.nbatches);
     for (auto &s : c->slots)
       if ((rc = alloc_slot(c, s))) break;

@@ -29,10 +29,12 @@ struct DevSA {
 };
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 
-// GHASH multiplication tables for one SA: powers H^1..H^8, 32 nibble
-// positions, 16 nibble values, 16-byte products in memory byte order.
-constexpr int kGhPowers = 8;
-constexpr uint32_t kGhTableBytes = kGhPowers * 32 * 16 * 16;   // 65536
+// GHASH multiplication tables for one SA: powers H^1..H^8 (index 0..7) and
+// H^16 (index 8), each 32 nibble positions x 16 nibble values x 16-byte
+// products in memory byte order (8 KiB per power).
+constexpr int kGhPowers = 9;
+constexpr uint32_t kGhPowerBytes = 32 * 16 * 16;                 // 8192
+constexpr uint32_t kGhTableBytes = kGhPowers * kGhPowerBytes;    // 73728
 
 // A chunk: up to kChunkRecs records of ONE session, processed by one
 // workgroup iteration of the GCM kernel.  rec positions index `order`
@@ -42,7 +44,7 @@ struct Chunk {
   uint32_t sa;
   uint32_t start;
   uint32_t count;
-  uint32_t cls;     // size class (planner); informational
+  uint32_t cls;     // size class 0..3 (GCM), 4 = invalid-session or ETA chunk
 };
 
 struct GcmParams {
@@ -51,7 +53,7 @@ struct GcmParams {
   const espgpu_desc *desc;
   const uint32_t *order;          // planner permutation or nullptr
   const Chunk *chunks;            // explicit chunk list, or nullptr (implicit)
-  const uint32_t *nchunks;        // device count of explicit chunks
+  const uint32_t *nchunks;        // [0] = GCM (+invalid) chunks, [1] = all chunks
   uint32_t n;                     // number of descriptors (implicit mode)
   const DevSA *sas;
   const uint8_t *gtab;            // [slot][65536]
@@ -68,6 +70,10 @@ struct EtaParams {
   uint8_t *arena;
   uint8_t *out;
   const espgpu_desc *desc;
+  const uint32_t *order;          // planner permutation or nullptr (implicit)
+  const Chunk *chunks;            // ETA chunks are [nchunks[0], nchunks[1])
+  const uint32_t *nchunks;
+  uint32_t *queue;                // [0] ticket, [1] retired waves (self-resetting)
   uint32_t n;
   const DevSA *sas;
   const uint2 *tpair;             // encryption pair table
@@ -78,12 +84,12 @@ struct EtaParams {
 };
 
 // Launchers (defined in the .hip files, called by espgpu.cpp).
-int gcm_set_sbox(const uint8_t *sbox256);
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream);
 int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream);
 size_t plan_workspace_words(uint32_t nsas);
+uint32_t plan_max_chunks(uint32_t n, uint32_t nsas);
 
 }  // namespace espgpu

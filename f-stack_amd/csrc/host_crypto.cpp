@@ -152,10 +152,12 @@ void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
 }
 
 void ghash_tables(const uint8_t h[16], uint8_t *out) {
-  uint8_t pw[8][16];
+  // powers H^1..H^8 at table index 0..7, H^16 at index 8
+  uint8_t pw[9][16];
   memcpy(pw[0], h, 16);
   for (int p = 1; p < 8; ++p) gf128_mul(pw[p - 1], h, pw[p]);
-  for (int p = 0; p < 8; ++p) {
+  gf128_mul(pw[7], pw[7], pw[8]);
+  for (int p = 0; p < 9; ++p) {
     // products of every single-bit block with H^(p+1)
     uint8_t bit[128][16];
     for (int b = 0; b < 128; ++b) {

@@ -26,7 +26,7 @@ void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
 
 // 64 KiB GHASH table set for the GCM kernel: powers H^1..H^8, per nibble
 // position j (byte j>>1, low nibble if j even), per nibble value.
-void ghash_tables(const uint8_t h[16], uint8_t *out65536);
+void ghash_tables(const uint8_t h[16], uint8_t *out);   // kGhTableBytes: H^1..H^8, H^16
 
 // SHA-1 compression of one 64-byte block into state h[5].
 void sha1_compress(uint32_t h[5], const uint8_t block[64]);

@@ -8,10 +8,13 @@
 //                and chunk offsets; writes the chunk list and its length
 //   plan_scatter per-workgroup LDS ranks + one global range reservation per
 //                non-empty key -> order[] (a permutation of descriptor ids)
-// Keys: [0, 4*nsas) = GCM records (class-major, largest class first), 4*nsas = records of ETA
-// sessions (not chunked: the ETA kernel walks descriptors directly),
-// 4*nsas+1 = records with no valid session (chunked with sa = ~0 so the GCM
-// kernel marks them EINVAL).  Cost: two passes over the 16-byte descriptors.
+// Keys: [0, 4*nsas) = GCM records (class-major, largest class first),
+// 4*nsas = records with no valid session (chunked with sa = ~0 so the GCM
+// kernel marks them EINVAL), 4*nsas+1+s = records of ETA session s.  GCM and
+// invalid keys make 128-record chunks, ETA keys 64-record (one wave) chunks;
+// chunks are emitted in key order, so nchunks[0] = the GCM kernel's share and
+// [nchunks[0], nchunks[1]) the ETA kernel's.  Cost: two passes over the
+// 16-byte descriptors.
 #include <hip/hip_runtime.h>
 
 #include "espgpu_internal.h"
@@ -35,20 +38,22 @@ __device__ __forceinline__ uint32_t size_class(uint32_t len) {
 
 __device__ __forceinline__ uint32_t key_of(const espgpu_desc &d, const DevSA *sas, uint32_t nsas) {
   const uint32_t sa = d.sa;
-  if (sa >= nsas) return 4 * nsas + 1;
+  if (sa >= nsas) return 4 * nsas;
   const uint32_t mode = sas[sa].mode;
-  if (mode == ESPGPU_CSP_MODE_ETA) return 4 * nsas;
-  if (mode != ESPGPU_CSP_MODE_AEAD) return 4 * nsas + 1;
-  // largest class first: with the GCM kernel's dynamic chunk queue this is
+  if (mode == ESPGPU_CSP_MODE_ETA) return 4 * nsas + 1 + sa;
+  if (mode != ESPGPU_CSP_MODE_AEAD) return 4 * nsas;
+  // largest class first: with the kernels' dynamic chunk queues this is
   // longest-processing-time-first scheduling
   return (3u - size_class(d.len)) * nsas + sa;
 }
+
+__host__ __device__ constexpr uint32_t num_keys(uint32_t nsas) { return 5 * nsas + 1; }
 
 __global__ __launch_bounds__(PWG) void plan_count(const espgpu_desc *desc, uint32_t n,
                                                   const DevSA *sas, uint32_t nsas,
                                                   uint32_t *gcnt) {
   __shared__ uint32_t hist[kMaxLdsKeys];
-  const uint32_t nkeys = 4 * nsas + 2;
+  const uint32_t nkeys = num_keys(nsas);
   for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) hist[k] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * TILE;
@@ -67,14 +72,17 @@ __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t 
                                                  uint32_t *gcur, Chunk *chunks,
                                                  uint32_t *nchunks, uint32_t max_chunks) {
   __shared__ uint32_t s_rec[PWG], s_chk[PWG];
-  const uint32_t nkeys = 4 * nsas + 2;
+  const uint32_t nkeys = num_keys(nsas);
   const uint32_t per = (nkeys + PWG - 1) / PWG;
   const uint32_t k0 = threadIdx.x * per, k1 = min(nkeys, k0 + per);
-  auto is_chunked = [&](uint32_t k) { return k != 4 * nsas; };
-  uint32_t r = 0, c = 0;
+  const uint32_t eta0 = 4 * nsas + 1;                       // first ETA key
+  auto recs_per_chunk = [&](uint32_t k) { return k >= eta0 ? 64u : (uint32_t)kChunkRecs; };
+  uint32_t r = 0, c = 0, cg = 0;
   for (uint32_t k = k0; k < k1; ++k) {
     r += gcnt[k];
-    if (is_chunked(k)) c += (gcnt[k] + kChunkRecs - 1) / kChunkRecs;
+    const uint32_t nc = (gcnt[k] + recs_per_chunk(k) - 1) / recs_per_chunk(k);
+    c += nc;
+    if (k < eta0) cg += nc;
   }
   s_rec[threadIdx.x] = r;
   s_chk[threadIdx.x] = c;
@@ -89,27 +97,31 @@ __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t 
     __syncthreads();
   }
   uint32_t roff = s_rec[threadIdx.x] - r, coff = s_chk[threadIdx.x] - c;
+  // the thread holding key eta0 (or the first one past the GCM keys) knows
+  // where the ETA chunks begin
+  if (k0 <= eta0 && eta0 < k1) nchunks[0] = min(coff + cg, max_chunks);
   for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t cnt = gcnt[k];
+    const uint32_t cnt = gcnt[k], rpc = recs_per_chunk(k);
     gcur[k] = roff;
-    if (is_chunked(k)) {
-      const uint32_t sa = (k == 4 * nsas + 1) ? 0xffffffffu : k % nsas;
-      const uint32_t cls = (k == 4 * nsas + 1) ? 0u : 3u - k / nsas;
-      for (uint32_t j = 0; j * kChunkRecs < cnt; ++j, ++coff) {
-        if (coff < max_chunks)
-          chunks[coff] = Chunk{sa, roff + j * kChunkRecs, min((uint32_t)kChunkRecs, cnt - j * kChunkRecs), cls};
-      }
+    const uint32_t sa = k == 4 * nsas ? 0xffffffffu : (k >= eta0 ? k - eta0 : k % nsas);
+    const uint32_t cls = k >= 4 * nsas ? 4u : 3u - k / nsas;
+    for (uint32_t j = 0; j * rpc < cnt; ++j, ++coff) {
+      if (coff < max_chunks)
+        chunks[coff] = Chunk{sa, roff + j * rpc, min(rpc, cnt - j * rpc), cls};
     }
     roff += cnt;
   }
-  if (threadIdx.x == PWG - 1) *nchunks = min(s_chk[PWG - 1], max_chunks);
+  if (threadIdx.x == PWG - 1) {
+    nchunks[1] = min(s_chk[PWG - 1], max_chunks);
+    if (eta0 >= nkeys) nchunks[0] = nchunks[1];             // no sessions: no ETA keys
+  }
 }
 
 __global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uint32_t n,
                                                     const DevSA *sas, uint32_t nsas,
                                                     uint32_t *gcur, uint32_t *order) {
   __shared__ uint32_t hist[kMaxLdsKeys], lbase[kMaxLdsKeys];
-  const uint32_t nkeys = 4 * nsas + 2;
+  const uint32_t nkeys = num_keys(nsas);
   for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) hist[k] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * TILE;
@@ -137,13 +149,14 @@ __global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uin
 }  // namespace
 
 // gcnt[nkeys] + gcur[nkeys]
-size_t plan_workspace_words(uint32_t nsas) { return 2 * (size_t)(4 * nsas + 2); }
+size_t plan_workspace_words(uint32_t nsas) { return 2 * (size_t)num_keys(nsas); }
+uint32_t plan_max_chunks(uint32_t n, uint32_t nsas) { return n / 64 + num_keys(nsas) + 8; }
 
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const uint32_t nkeys = 4 * nsas + 2;
+  const uint32_t nkeys = num_keys(nsas);
   if (nkeys > kMaxLdsKeys) return -1;     // caller must pre-group (ESPGPU_BATCH_GROUPED)
   uint32_t *gcnt = d_work, *gcur = d_work + nkeys;
   if (hipMemsetAsync(gcnt, 0, nkeys * sizeof(uint32_t), st) != hipSuccess) return -1;

@@ -339,3 +339,50 @@ def test_host_pipeline_vs_oracle(drv, chunk):
     assert (h_out.numpy()[m] == plain[m]).all()
     for s in sids:
         drv.freesession(s)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_kernel_variants_vs_oracle(drv, variant):
+    """Every GCM kernel variant (workgroup size x paired steps) decrypts,
+    verifies and encrypts bit-exactly, incl. records crossing counter 256."""
+    from espgpu.batch import decrypt_batch, encrypt_batch
+    rng = np.random.default_rng(700 + variant)
+    sas = [GcmSA(rng, 16), GcmSA(rng, 32, esn=True)]
+    sids = _sessions(drv, sas)
+    n = 1200
+    sa_idx = rng.integers(0, 2, n)
+    cts = rng.choice([4, 12, 100, 204, 1448, 4000, 8948, 8940], n)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts,
+                                         esn_hi=rng.integers(0, 2**32, n, dtype=np.uint32))
+    bad = ct.copy()
+    flip = rng.random(n) < 0.05
+    for i in np.nonzero(flip)[0]:
+        bad[int(descs["off4"][i]) * 4 + 16 + int(rng.integers(0, int(descs["len"][i]) - 16))] ^= 0x10
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_variant", variant) == 0
+    try:
+        for inplace in (False, True):
+            arena = _dev(bad)
+            out = arena if inplace else torch.zeros_like(arena)
+            st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+            decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out)
+            torch.cuda.synchronize()
+            got = st.cpu().numpy()
+            assert (got == ref_st).all(), (inplace, np.nonzero(got != ref_st)[0][:10])
+            m = payload_mask(descs[got == 0], len(bad))
+            assert (out.cpu().numpy()[m] == ref_out[m]).all()
+            if inplace:
+                mb = payload_mask(descs[got != 0], len(bad), 0, 0)
+                assert (out.cpu().numpy()[mb] == bad[mb]).all()
+        arena = _dev(plain)
+        st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        encrypt_batch(drv, arena, _descs_dev(d), n, st)
+        torch.cuda.synchronize()
+        assert (st.cpu().numpy() == 0).all()
+        assert (arena.cpu().numpy() == ct).all()
+    finally:
+        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_variant", 0)
+        for s in sids:
+            drv.freesession(s)
