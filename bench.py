@@ -25,6 +25,8 @@ sys.path.insert(0, os.path.join(ROOT, "f-stack_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CONFIGS = {
+    "cfg0": dict(workload="cfg0: 64K x 64B ESP AES-128-GCM decrypt, single SA", packets=1 << 16,
+                 pkt=64, skip=20, klen=16, nsa=1, mixed=False, alg="gcm"),
     "cfg1": dict(workload="cfg1: 1M x 1500B ESP AES-128-GCM decrypt, single SA", packets=1 << 20,
                  pkt=1500, skip=20, klen=16, nsa=1, mixed=False, alg="gcm"),
     "cfg2": dict(workload="cfg2: 1M x {64,256,1500,9000}B mixed-MTU ESP AES-128-GCM decrypt, 1K SAs",

@@ -387,8 +387,9 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 
 }  // namespace
 
-// Decrypt runs 512-thread workgroups (2 waves/SIMD, up to 256 VGPRs: the
-// unrolled SHA-1 schedule needs ~170 and spills at 128); encrypt runs 1024.
+// Decrypt runs 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the
+// unrolled SHA-1 schedule needs ~150 and spills at 128), one workgroup per CU
+// (96 KiB LDS); encrypt runs 1024.
 int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
@@ -396,9 +397,9 @@ int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream) {
   if (encrypt)
     hipLaunchKernelGGL((eta_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, p);
   else if (two_pass)
-    hipLaunchKernelGGL((eta_kernel<2, 512>), dim3(grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL((eta_kernel<2, 768>), dim3(grid), dim3(768), 0, st, p);
   else
-    hipLaunchKernelGGL((eta_kernel<0, 512>), dim3(grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL((eta_kernel<0, 768>), dim3(grid), dim3(768), 0, st, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -97,7 +97,7 @@ struct espgpu_ctx {
   std::vector<espgpu_completion> ready;   // host-side completions (EINVAL etc.)
   espgpu_stats stats{};
   float last_ms = 0.f;
-  int gcm_variant = 0;       // tuning: see launch_gcm
+  int gcm_variant = 2;       // tuning: see launch_gcm (default: 1024-thread WGs, paired steps)
   std::string err;
 };
 

@@ -383,6 +383,6 @@ def test_kernel_variants_vs_oracle(drv, variant):
         assert (st.cpu().numpy() == 0).all()
         assert (arena.cpu().numpy() == ct).all()
     finally:
-        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_variant", 0)
+        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_variant", 2)
         for s in sids:
             drv.freesession(s)
