@@ -45,7 +45,7 @@ def main():
     dominant = max(ks, key=lambda k: ks[k]["pct"])
     key = "gcm_kernel<0>" if "gcm_kernel<0>" in dominant else dominant
     c = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_sq3"):
         c.update(counters(d, sub, key))
     res = {"tag": tag, "config": cfg, "dominant_kernel": dominant, "kernels": ks, "counters": c}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:

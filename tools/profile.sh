@@ -14,4 +14,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_write.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_sq" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_sq.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d "$OUT/pmc_sq2" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_sq2.log" 2>&1 || echo "pmc_sq2 pass failed (see log)"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM -d "$OUT/pmc_sq3" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_sq3.log" 2>&1 || echo "pmc_sq3 pass failed (see log)"
 echo "profile $TAG done"
