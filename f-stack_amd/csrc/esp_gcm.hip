@@ -33,6 +33,7 @@
 //    plaintext + status byte.
 #include <hip/hip_runtime.h>
 
+#include "bsaes.h"
 #include "espgpu_internal.h"
 
 namespace espgpu {
@@ -73,36 +74,23 @@ __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
   *reinterpret_cast<U4 *>(p) = u;
 }
 
-// Keep the first `rem` bytes (1..16) of a 16-byte block, zero the rest.
+// Keep the first `rem` bytes of a 16-byte block, zero the rest.  Valid ESP
+// payloads are 4-byte multiples (the kernel rejects len % 4 != 0, as
+// esp_output pads to 4, xform_esp.c:710-716), so rem is 4, 8, 12 or >= 16.
 __device__ __forceinline__ uint4 mask_block(uint4 v, int rem) {
-  if (rem >= 16) return v;
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    int b = rem - 4 * k;
-    uint32_t m = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
-    w[k] &= m;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  return make_uint4(v.x, rem > 4 ? v.y : 0u, rem > 8 ? v.z : 0u, rem > 12 ? v.w : 0u);
 }
 
-// Store the first `rem` bytes of v (ESP payloads are 4-byte multiples; the
-// byte tail keeps generic GCM lengths exact).
+// Store the first `rem` bytes (a multiple of 4) of v.
 __device__ __forceinline__ void st_partial(uint8_t *p, uint4 v, int rem) {
   if (rem >= 16) {
     st16(p, v);
     return;
   }
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    int b = rem - 4 * k;
-    if (b >= 4) {
-      *reinterpret_cast<uint32_t *>(p + 4 * k) = w[k];
-    } else if (b > 0) {
-      for (int t = 0; t < b; ++t) p[4 * k + t] = (uint8_t)(w[k] >> (8 * t));
-    }
-  }
+  uint32_t *q = reinterpret_cast<uint32_t *>(p);
+  q[0] = v.x;
+  if (rem > 4) q[1] = v.y;
+  if (rem > 8) q[2] = v.z;
 }
 
 // ---- AES (rijndaelEncrypt, rijndael-alg-fst.c:863-1042) on the pair table ----
@@ -146,7 +134,13 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
 // results on purpose, to split the kernel's time: bit1 skips the GHASH
 // multiplies of the main loop, bit2 the AES rounds after round 2.
 __device__ uint32_t g_opts;
+// Compiled in only for measurement builds (make KNOBS=1): a scalar load and
+// branch per use would otherwise sit in the hot loop.
+#ifdef ESPGPU_KNOBS
 __device__ __forceinline__ uint32_t gopts() { return *(const __attribute__((address_space(4))) uint32_t *)(const void *)&g_opts; }
+#else
+__device__ __forceinline__ constexpr uint32_t gopts() { return 0; }
+#endif
 
 // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
 // words directly; the last round key is stored byte-swapped.
@@ -235,10 +229,14 @@ __device__ __forceinline__ uint4 aes_ctr(const CtrCache &cc, uint32_t ctr, uint3
 
 // Two counter blocks (both covered by the cache) interleaved round by round:
 // each round issues 32 independent LDS lookups before the wave waits, halving
-// the dependent LDS round trips per block.
+// the dependent LDS round trips per block.  KR > 0: the last KR rounds of the
+// pair run bitsliced on the VALU (bsaes.h), taking 16*KR LDS lookups per block
+// off the LDS, which is the kernel's bottleneck; their plane round keys are in
+// DevSA.dk (scalar loads).
+template <int KR>
 __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32_t cb, uint32_t rk3,
-                                         int nr, rkptr rk, const uint8_t *lds, uint32_t slot,
-                                         uint4 &ka, uint4 &kb) {
+                                         int nr, rkptr rk, rkptr bsk, const uint8_t *lds,
+                                         uint32_t slot, uint4 &ka, uint4 &kb) {
   const uint32_t ta = cc.K0 ^ ror16(te1(lds, tpa(ca ^ rk3, slot, 0)));
   const uint32_t tb = cc.K0 ^ ror16(te1(lds, tpa(cb ^ rk3, slot, 0)));
   uint32_t a0 = cc.L0 ^ te0(lds, tpa(ta, slot, 3)), b0 = cc.L0 ^ te0(lds, tpa(tb, slot, 3));
@@ -252,15 +250,23 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll 1
-  for (int r = 3; r < nr; ++r) {
+  for (int r = 3; r < nr - KR + (KR == 0 ? 0 : 1); ++r) {
     const uint4 k = ldk4(rk + 4 * r);
     aes_round(a0, a1, a2, a3, k, lds, slot);
     aes_round(b0, b1, b2, b3, k, lds, slot);
     __builtin_amdgcn_sched_barrier(0);
   }
-  const uint4 kl = ldk4(rk + 4 * nr);
-  ka = aes_last(a0, a1, a2, a3, kl, lds, slot);
-  kb = aes_last(b0, b1, b2, b3, kl, lds, slot);
+  if (KR == 0) {
+    const uint4 kl = ldk4(rk + 4 * nr);
+    ka = aes_last(a0, a1, a2, a3, kl, lds, slot);
+    kb = aes_last(b0, b1, b2, b3, kl, lds, slot);
+  } else {
+    const uint32_t sa[4] = {a0, a1, a2, a3}, sb[4] = {b0, b1, b2, b3};
+    uint32_t oa[4], ob[4];
+    bs::tail_rounds<(KR > 0 ? KR : 1)>(sa, sb, bsk + 8 * (4 - KR), oa, ob);
+    ka = make_uint4(bswap32(oa[0]), bswap32(oa[1]), bswap32(oa[2]), bswap32(oa[3]));
+    kb = make_uint4(bswap32(ob[0]), bswap32(ob[1]), bswap32(ob[2]), bswap32(ob[3]));
+  }
 }
 
 // ---- GHASH multiply by a fixed power (gf128_mul, gfmult.c:219-229) ----------
@@ -352,11 +358,12 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 1: encrypt in place + ICV
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
 // PAIR: steps m, m+1 of a lane run together (2 independent AES blocks, and
-// Y <- Y*H^16 ^ B_m*H^8 ^ B_m+1 as 2 independent GHASH products).
-template <int MODE, bool PAIR>
+// Y <- Y*H^16 ^ B_m*H^8 ^ B_m+1 as 2 independent GHASH products); KR: the
+// pair's last KR AES rounds are bitsliced (0 = all T-table).
+template <int MODE, bool PAIR, int KR>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di,
                                                    bool have, uint32_t sa, uint32_t sa_flags,
-                                                   uint32_t mlen, int nr, rkptr rk) {
+                                                   uint32_t mlen, int nr, rkptr rk, rkptr bsk) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
@@ -432,7 +439,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         if (hca) Ca = ld16(rec + 16 * i);
         if (hcb) Cb = ld16(rec + 16 * ib);
         uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
-        if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+        if (MODE != 2) aes_ctr2<KR>(cc, ca, cb, rk3, nr, rk, bsk, lds, slot, ka, kb);
         const uint4 Ba = block_in(i, hca, Ca, ka);
         const uint4 Bb = block_in(ib, hcb, Cb, kb);
         if (!(gopts() & 2)) {
@@ -511,7 +518,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
-template <int MODE, int WG, bool PAIR>
+template <int MODE, int WG, bool PAIR, int KR>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -580,8 +587,9 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         if (mode == 0 && have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
         continue;
       }
-      do_group<MODE, PAIR>(p, lds, di, have, sa, flags, mlen, (int)nr,
-                           (rkptr)(const void *)(p.sas[sa].rk));
+      do_group<MODE, PAIR, KR>(p, lds, di, have, sa, flags, mlen, (int)nr,
+                               (rkptr)(const void *)(p.sas[sa].rk),
+                               (rkptr)(const void *)(p.sas[sa].dk));
     }
   }
   // Every workgroup leaves the loop after drawing exactly one ticket >= nch,
@@ -595,21 +603,29 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
 }  // namespace
 
 // variant: bit0 = 512-thread workgroups (2 waves/SIMD, 256 VGPRs) instead of
-// 1024 (4 waves/SIMD, 128 VGPRs); bit1 = PAIR (two steps per lane at once).
+// 1024 (4 waves/SIMD, 128 VGPRs); bit1 = PAIR (two steps per lane at once);
+// bits 2-3 (PAIR, 1024 only) = bitsliced tail rounds KR = 0, 2, 3, 4.
 template <int MODE>
 static void launch_mode(const GcmParams &p, int variant, int grid, hipStream_t st) {
+  const int kr = (variant >> 2) & 3;
   switch (variant & 3) {
-    case 0: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, false>), dim3(grid), dim3(1024), 0, st, p); break;
-    case 1: hipLaunchKernelGGL((gcm_kernel<MODE, 512, false>), dim3(grid), dim3(512), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true>), dim3(grid), dim3(1024), 0, st, p); break;
-    default: hipLaunchKernelGGL((gcm_kernel<MODE, 512, true>), dim3(grid), dim3(512), 0, st, p); break;
+    case 0: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, false, 0>), dim3(grid), dim3(1024), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((gcm_kernel<MODE, 512, false, 0>), dim3(grid), dim3(512), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((gcm_kernel<MODE, 512, true, 0>), dim3(grid), dim3(512), 0, st, p); break;
+    default:
+      switch (kr) {
+        case 0: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 0>), dim3(grid), dim3(1024), 0, st, p); break;
+        case 1: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 2>), dim3(grid), dim3(1024), 0, st, p); break;
+        case 2: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 3>), dim3(grid), dim3(1024), 0, st, p); break;
+        default: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 4>), dim3(grid), dim3(1024), 0, st, p); break;
+      }
   }
 }
 
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   static int cur_opts = -1;
-  const uint32_t opts = (uint32_t)variant >> 2;
+  const uint32_t opts = (uint32_t)variant >> 4;
   if ((int)opts != cur_opts) {
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_opts), &opts, 4, 0, hipMemcpyHostToDevice, st);
     hipStreamSynchronize(st);

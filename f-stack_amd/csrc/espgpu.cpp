@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "espgpu.h"
+#include "bsaes.h"
 #include "espgpu_internal.h"
 #include "host_crypto.h"
 
@@ -346,14 +347,16 @@ int espgpu_probesession(const espgpu_session_params *csp) {
       if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_NIST_GCM_16 || !aes_klen) return EINVAL;
       if (csp->csp_ivlen != 12) return EINVAL;                 // cryptosoft.c:1093
       if (csp->csp_auth_alg != 0 || csp->csp_auth_klen != 0) return EINVAL;
-      if (csp->csp_auth_mlen > 16) return EINVAL;
+      // ICVs of 8/12/16 bytes (RFC 4106 s3.3); the kernels move whole dwords,
+      // so other truncations are left to cryptosoft (probe EINVAL)
+      if (csp->csp_auth_mlen > 16 || (csp->csp_auth_mlen & 3)) return EINVAL;
       if (csp->csp_flags & ESPGPU_CSP_F_ESN) return EINVAL;    // ESN for GCM = SEPARATE_AAD
       return ESPGPU_PROBE_HARDWARE;
     case ESPGPU_CSP_MODE_ETA:
       if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC || !aes_klen) return EINVAL;
       if (csp->csp_ivlen != 16) return EINVAL;
       if (csp->csp_auth_alg != ESPGPU_CRYPTO_SHA1_HMAC || csp->csp_auth_klen <= 0) return EINVAL;
-      if (csp->csp_auth_mlen > 20) return EINVAL;
+      if (csp->csp_auth_mlen > 20 || (csp->csp_auth_mlen & 3)) return EINVAL;
       if (csp->csp_flags & ESPGPU_CSP_F_SEPARATE_AAD) return EINVAL;
       return ESPGPU_PROBE_HARDWARE;
     default:
@@ -389,6 +392,7 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     for (int i = 0; i < 4; ++i) sa.rk[i] = rk[i];
     for (int i = 4; i < 4 * nr; ++i) sa.rk[i] = ror16(rk[i]);
     for (int i = 0; i < 4; ++i) sa.rk[4 * nr + i] = bswap(rk[4 * nr + i]);
+    bs::round_keys(rk, nr, 4, sa.dk);      // bitsliced tail: plane keys of the last 4 rounds
     uint8_t zero[16] = {0}, h[16];
     hc::aes_encrypt_block(rk, nr, zero, h);       // H = E_K(0^128), gmac.c:56-60
     std::vector<uint8_t> tabs(kGhTableBytes);

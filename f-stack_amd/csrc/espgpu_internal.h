@@ -11,7 +11,8 @@ namespace espgpu {
 // GCM: rk[] is the AES encryption schedule in "kernel form" for the pair-table
 //   round (see esp_gcm.hip):  rk[0..3] raw, rk[4r..4r+3] = ror16(rk) for the
 //   middle rounds, rk[4nr..] byte-swapped (the last round emits little-endian
-//   words).  The GHASH tables live in a separate 64 KiB-per-slot array.
+//   words); dk[0..31] = bitsliced plane keys of the last 4 rounds (bsaes.h).
+//   The GHASH tables live in a separate 72 KiB-per-slot array.
 // ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
 //   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
 //   = SHA-1 chaining state after one block of key^0x36 / key^0x5c

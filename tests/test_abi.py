@@ -39,6 +39,10 @@ def test_probesession_accepts_esp_gcm(klen):
     assert _probe(csp_mode=L.CSP_MODE_AEAD, csp_flags=L.CSP_F_SEPARATE_AAD, csp_ivlen=12,
                   csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16, csp_cipher_klen=klen,
                   csp_cipher_key=b"k" * klen) == L.CRYPTODEV_PROBE_HARDWARE
+    for mlen in (8, 12, 16):            # RFC 4106 ICV lengths
+        assert _probe(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16,
+                      csp_cipher_klen=klen, csp_cipher_key=b"k" * klen,
+                      csp_auth_mlen=mlen) == L.CRYPTODEV_PROBE_HARDWARE
 
 
 def test_probesession_accepts_esp_cbc_sha1():
@@ -58,6 +62,8 @@ def test_probesession_accepts_esp_cbc_sha1():
     dict(csp_mode=2, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16),                  # cipher-only
     dict(csp_mode=L.CSP_MODE_AEAD, csp_flags=0x1, csp_ivlen=12, csp_cipher_alg=25,
          csp_cipher_klen=16),                                                               # SEPARATE_OUTPUT
+    dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=25, csp_cipher_klen=16,
+         csp_auth_mlen=10),                                                                 # ICV not dwords
 ])
 def test_probesession_rejects(kw):
     assert _probe(**kw) == L.EINVAL
