@@ -40,11 +40,11 @@ namespace espgpu {
 
 namespace {
 
-constexpr uint32_t LDS_TP = 0;          // 256 entries x 32 lane slots x 8 B
-constexpr uint32_t LDS_GT = 65536;      // GHASH tables: H^1..H^8, H^16 (8 KiB each)
-constexpr uint32_t LDS_BYTES = LDS_GT + kGhTableBytes;
-constexpr uint32_t PW8 = LDS_GT + 7 * kGhPowerBytes;    // H^8
-constexpr uint32_t PW16 = LDS_GT + 8 * kGhPowerBytes;   // H^16
+// LDS: the 8-bit H^8 GHASH table at 0 (so its 16 position offsets p*4096
+// fit the DS instructions' 16-bit immediate), the AES T-table at 64 KiB.
+constexpr uint32_t LDS_GT = 0;          // H^8, 16 positions x 256 values x 16 B
+constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
+constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
 constexpr int S = 8;                    // lanes per record
 
 // Round keys are read through the constant address space: uniform loads from
@@ -95,15 +95,16 @@ __device__ __forceinline__ void st_partial(uint8_t *p, uint4 v, int rem) {
 
 // ---- AES (rijndaelEncrypt, rijndael-alg-fst.c:863-1042) on the pair table ----
 
-// T-table layout (64 KiB): entry x occupies 256 bytes = Te0[x] replicated in
-// 32 lane slots (bytes 0..127) followed by Te1[x] = ror8(Te0[x]) in 32 slots
-// (bytes 128..255).  Lane L reads slot L&31, so for ds_read_b32 (32 banks,
-// bank = dword index mod 32, 32-lane groups) every lane of a group hits its
-// own bank whatever the indices: conflict-free.  The address of Te0[byte k of
-// w] for this lane is ONE v_perm_b32: byte0 = (L&31)*4, byte1 = w.byte k; Te1
-// is the same address + 128 (DS immediate offset).
+// T-table layout (64 KiB at LDS_TP): entry x occupies 256 bytes = Te0[x]
+// replicated in 32 lane slots (bytes 0..127) followed by Te1[x] =
+// ror8(Te0[x]) in 32 slots (bytes 128..255).  Lane L reads slot L&31, so for
+// ds_read_b32 (32 banks, bank = dword index mod 32, 32-lane groups) every lane
+// of a group hits its own bank whatever the indices: conflict-free.  The
+// address of Te0[byte k of w] for this lane is ONE v_perm_b32: byte0 =
+// (L&31)*4 and byte2 = LDS_TP>>16 from `slot`, byte1 = w.byte k; Te1 is the
+// same address + 128 (DS immediate offset).
 __device__ __forceinline__ uint32_t tpa(uint32_t w, uint32_t slot, int k) {
-  return perm(w, slot, 0x0c0c0000u | ((4u + (uint32_t)k) << 8));
+  return perm(w, slot, 0x0c020000u | ((4u + (uint32_t)k) << 8));
 }
 __device__ __forceinline__ uint32_t te0(const uint8_t *lds, uint32_t a) {
   return *reinterpret_cast<const uint32_t *>(lds + a);
@@ -269,27 +270,51 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32
   }
 }
 
-// ---- GHASH multiply by a fixed power (gf128_mul, gfmult.c:219-229) ----------
-// pb = LDS byte address of the power's 8 KiB table (low byte 0, < 2^24).
-// Nibble position j = 8k + 2q (+1 for the high nibble) of word k, byte q.
-__device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds) {
+// ---- GHASH multiply by a fixed power (gf_mul, gfmult.c:219-229) ----------
+// Y * H^8 with 8-bit tables in LDS: 16 lookups (one per byte position p, the
+// row p*4096 + byte*16), XOR-accumulated.  The address is one shift of the
+// byte; the position offset is the DS immediate.  Entry v of a row sits in
+// bank group v mod 16, so lanes of a ds_read_b128 group conflict only when
+// their bytes differ but agree mod 16.
+__device__ __forceinline__ uint4 gf_mul8(uint4 x, const uint8_t *lds) {
   uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-  // One 32-bit word (8 nibble positions) per iteration; the loop is kept
-  // rolled so at most 8 lookups (32 VGPRs) are in flight per wave, and the
-  // word in use is rotated into w instead of indexing an array (which would
-  // go to scratch).  pb advances 8 position tables (2 KiB) per word.
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      const uint32_t a = ((w[k] >> (8 * q)) & 0xffu) << 4;
+      const uint32_t b = ((w[k] >> (8 * q + 8)) & 0xffu) << 4;
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + LDS_GT + (4 * k + q) * 4096 + a);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + LDS_GT + (4 * k + q + 1) * 4096 + b);
+      r0 = xor3(r0, e.x, f.x);
+      r1 = xor3(r1, e.y, f.y);
+      r2 = xor3(r2, e.z, f.z);
+      r3 = xor3(r3, e.w, f.w);
+    }
+    // Materialize the partial sums here: otherwise the XORs sink into the
+    // caller's `if (m < M)` and all 16 rows (64 VGPRs) stay live -> spills.
+    asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
+  }
+  return make_uint4(r0, r1, r2, r3);
+}
+
+// Y * H^e with the 4-bit table of that power in global memory (t = its 8 KiB:
+// nibble position j (byte j>>1, low nibble if j even), value n at j*256+n*16).
+// Used once per record per lane (the final x H^(8-l)), where the power differs
+// per lane: from LDS that would be bank conflicts, from L2 it is a gather.
+__device__ __forceinline__ uint4 gf_mul4_global(uint4 x, const uint8_t *t) {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
   uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
+  // rolled over the 4 words (8 positions, 2 KiB of table each): the table
+  // addresses stay one pointer instead of 16 hoisted 64-bit ones
 #pragma unroll 1
   for (int k = 0; k < 4; ++k) {
-    const uint32_t hi = w & 0xF0F0F0F0u;           // high nibble * 16, per byte
-    const uint32_t lo = (w << 4) & 0xF0F0F0F0u;    // low nibble * 16, per byte
+    const uint32_t hi = w & 0xF0F0F0F0u, lo = (w << 4) & 0xF0F0F0F0u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t sel = 0x0c060500u | (uint32_t)q;
-      const uint32_t alo = perm(pb, lo, sel);
-      const uint32_t ahi = perm(pb, hi, sel);
-      const uint4 e = *reinterpret_cast<const uint4 *>(lds + alo + (2 * q) * 256);
-      const uint4 f = *reinterpret_cast<const uint4 *>(lds + ahi + (2 * q + 1) * 256);
+      const uint4 e = *reinterpret_cast<const uint4 *>(t + (2 * q) * 256 + ((lo >> (8 * q)) & 0xffu));
+      const uint4 f = *reinterpret_cast<const uint4 *>(t + (2 * q + 1) * 256 + ((hi >> (8 * q)) & 0xffu));
       r0 = xor3(r0, e.x, f.x);
       r1 = xor3(r1, e.y, f.y);
       r2 = xor3(r2, e.z, f.z);
@@ -298,49 +323,9 @@ __device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds
     w = w1;
     w1 = w2;
     w2 = w3;
-    pb += 8 * 256;
+    t += 8 * 256;
   }
   return make_uint4(r0, r1, r2, r3);
-}
-
-// Two independent products x * P and y * Q in one rolled word loop: 4 table
-// rows in flight per lookup group instead of 2.
-__device__ __forceinline__ void gf_mul2(uint4 x, uint32_t px, uint4 y, uint32_t py,
-                                        const uint8_t *lds, uint4 &rx, uint4 &ry) {
-  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-  uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
-  uint32_t v = y.x, v1 = y.y, v2 = y.z, v3 = y.w;
-#pragma unroll 1
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t hw = w & 0xF0F0F0F0u, lw = (w << 4) & 0xF0F0F0F0u;
-    const uint32_t hv = v & 0xF0F0F0F0u, lv = (v << 4) & 0xF0F0F0F0u;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t sel = 0x0c060500u | (uint32_t)q;
-      const uint4 e = *reinterpret_cast<const uint4 *>(lds + perm(px, lw, sel) + (2 * q) * 256);
-      const uint4 f = *reinterpret_cast<const uint4 *>(lds + perm(px, hw, sel) + (2 * q + 1) * 256);
-      const uint4 g = *reinterpret_cast<const uint4 *>(lds + perm(py, lv, sel) + (2 * q) * 256);
-      const uint4 h = *reinterpret_cast<const uint4 *>(lds + perm(py, hv, sel) + (2 * q + 1) * 256);
-      a0 = xor3(a0, e.x, f.x);
-      a1 = xor3(a1, e.y, f.y);
-      a2 = xor3(a2, e.z, f.z);
-      a3 = xor3(a3, e.w, f.w);
-      b0 = xor3(b0, g.x, h.x);
-      b1 = xor3(b1, g.y, h.y);
-      b2 = xor3(b2, g.z, h.z);
-      b3 = xor3(b3, g.w, h.w);
-    }
-    w = w1;
-    w1 = w2;
-    w2 = w3;
-    v = v1;
-    v1 = v2;
-    v2 = v3;
-    px += 8 * 256;
-    py += 8 * 256;
-  }
-  rx = make_uint4(a0, a1, a2, a3);
-  ry = make_uint4(b0, b1, b2, b3);
 }
 
 __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
@@ -366,7 +351,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
                                                    uint32_t mlen, int nr, rkptr rk, rkptr bsk) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
-  const uint32_t slot = (uint32_t)(lane & 31) * 4;
+  const uint32_t slot = ((uint32_t)(lane & 31) * 4) | (LDS_TP & 0xff0000u);
   const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
 
   // -- descriptor and record header ------------------------------------------
@@ -442,13 +427,12 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         if (MODE != 2) aes_ctr2<KR>(cc, ca, cb, rk3, nr, rk, bsk, lds, slot, ka, kb);
         const uint4 Ba = block_in(i, hca, Ca, ka);
         const uint4 Bb = block_in(ib, hcb, Cb, kb);
-        if (!(gopts() & 2)) {
-          // M >= m+2: Y = Y*H^16 ^ Ba*H^8 ^ Bb;  M == m+1: Y = Y*H^8 ^ Ba
-          const bool two = M >= m + 2;
-          uint4 P, Q;
-          gf_mul2(Y, two ? PW16 : PW8, Ba, PW8, lds, P, Q);
-          if (two) Y = xor4(xor4(P, Q), Bb);
-          else if (M == m + 1) Y = xor4(P, Ba);
+        const uint4 P = (gopts() & 2) ? Y : gf_mul8(Y, lds);
+        // M >= m+2: Y = (Y*H^8 ^ Ba)*H^8 ^ Bb;  M == m+1: Y = Y*H^8 ^ Ba
+        if (M >= m + 1) {
+          const uint4 Ym = xor4(P, Ba);
+          Y = Ym;
+          if (M >= m + 2) Y = xor4((gopts() & 2) ? Ym : gf_mul8(Ym, lds), Bb);
         }
         m += 2;
         continue;
@@ -463,7 +447,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
     uint4 ks = make_uint4(0, 0, 0, 0);
     if (m > 0 && !(gopts() & 2)) {
-      const uint4 Yn = gf_mul(Y, PW8, lds);
+      const uint4 Yn = gf_mul8(Y, lds);
       if (m < M) Y = Yn;
     }
     if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
@@ -478,7 +462,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     ++m;
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
-  uint4 Z = gf_mul(Y, LDS_GT + (uint32_t)(7 - l) * kGhPowerBytes, lds);
+  uint4 Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + kGh8Bytes +
+                                 (uint32_t)(7 - l) * kGhPowerBytes);
   Z = xor4(Z, shfl_xor4(Z, 1));
   Z = xor4(Z, shfl_xor4(Z, 2));
   Z = xor4(Z, shfl_xor4(Z, 4));
@@ -569,7 +554,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes);
         uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
 #pragma unroll 4
-        for (int q = tid; q < (int)(kGhTableBytes / 16); q += WG) dst[q] = src[q];
+        for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
       } else {
         mode = 0;
       }

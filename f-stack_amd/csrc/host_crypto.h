@@ -24,9 +24,10 @@ void aes_encrypt_block(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t
 // GF(2^128) product in GCM bit order (SP 800-38D Algorithm 1).
 void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
 
-// 64 KiB GHASH table set for the GCM kernel: powers H^1..H^8, per nibble
-// position j (byte j>>1, low nibble if j even), per nibble value.
-void ghash_tables(const uint8_t h[16], uint8_t *out);   // kGhTableBytes: H^1..H^8, H^16
+// GHASH table set for the GCM kernel (kGhTableBytes = 128 KiB): H^8 with
+// 8-bit indices (64 KiB, staged in LDS), then H^1..H^8 with 4-bit indices
+// (64 KiB, read from global memory by the per-record final multiply).
+void ghash_tables(const uint8_t h[16], uint8_t *out);
 
 // SHA-1 compression of one 64-byte block into state h[5].
 void sha1_compress(uint32_t h[5], const uint8_t block[64]);
