@@ -285,7 +285,10 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       const DevSA *s = sa < p.nsas ? p.sas + sa : nullptr;
       if (!s || s->mode != ESPGPU_CSP_MODE_ETA) {
         have = false;                                       // not ours (GCM kernel / EINVAL)
-        if (!s || s->mode == 0) p.status[di] = ESPGPU_EINVAL;
+        if (!s || s->mode == 0) {
+          p.status[di] = ESPGPU_EINVAL;
+          if (MODE != 1 && p.trailer) p.trailer[di] = 0;
+        }
       } else {
         const uint32_t mlen = s->mlen;
         const int pl = (int)len - 24 - (int)mlen;           // hlen 24, alen = mlen (12)
@@ -325,6 +328,9 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       continue;
     }
     if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+    // trailer word: 0 now for records that will not be decrypted; the lane
+    // decrypting a record's last block writes the others'
+    if (have && p.trailer && !(valid && ok)) p.trailer[di] = 0;
 
     // ---- decrypt: all of the wave's blocks of one session as one flat list ----
     // Records to decrypt (one session at a time, so the round keys stay
@@ -367,12 +373,15 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           }
         }
         const uint32_t ro = __shfl(off, j);
+        const uint32_t rpl = __shfl(plen, j), rdi = __shfl(di, j);
         if (f >= 0) {
           const uint32_t i = (uint32_t)f - sj;
           const uint8_t *rec = p.arena + ro;
           const uint4 c = ld16(rec + 24 + 16 * i);
           const uint4 prev = ld16(rec + 8 + 16 * i);         // C_{i-1}, or the IV for i = 0
-          st16(obase + ro + 24 + 16 * i, xor4(aes_dec(c, dk, nr, lds, slot), prev));
+          const uint4 pt = xor4(aes_dec(c, dk, nr, lds, slot), prev);
+          st16(obase + ro + 24 + 16 * i, pt);
+          if (p.trailer && i == rpl / 16 - 1) p.trailer[rdi] = esp_trailer_word(pt.w, rpl);
         }
       }
     }

@@ -393,6 +393,14 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
 
   // GHASH input block of GHASH index i (>= 1) given its ciphertext C and
   // keystream ks; stores the output block (MODE 0: plaintext, MODE 1: CT).
+  // fused esp_input_cb trailer word, from the lane holding the last CT block
+  uint32_t trl = 0;
+  const bool want_trl = MODE != 1 && p.trailer != nullptr;
+  auto note_trailer = [&](int i, uint4 pt, int rem) {
+    if (want_trl && i == nct)
+      trl = esp_trailer_word(rem >= 16 ? pt.w : (rem > 8 ? pt.z : (rem > 4 ? pt.y : pt.x)),
+                             (uint32_t)ct_len);
+  };
   auto block_in = [&](int i, bool has_ct, uint4 C, uint4 ks) -> uint4 {
     if (has_ct) {
       const int c = i - 1;
@@ -402,7 +410,11 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         st_partial(orec + 16 + 16 * c, o, rem);
         return mask_block(o, rem);
       }
-      if (MODE == 0) st_partial(orec + 16 + 16 * c, xor4(C, ks), rem);
+      if (MODE == 0) {
+        const uint4 pt = xor4(C, ks);
+        st_partial(orec + 16 + 16 * c, pt, rem);
+        note_trailer(i, pt, rem);
+      }
       return mask_block(C, rem);
     }
     if (valid && i == N - 1)                                     // length block
@@ -495,9 +507,18 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       if (run && i >= 1 && i <= nct) {
         const int c = i - 1;
         const uint4 C = ld16(rec + 16 + 16 * c);
-        st_partial(rec + 16 + 16 * c, xor4(C, ks), ct_len - 16 * c);
+        const uint4 pt = xor4(C, ks);
+        st_partial(rec + 16 + 16 * c, pt, ct_len - 16 * c);
+        note_trailer(i, pt, ct_len - 16 * c);
       }
     }
+  }
+  if (want_trl) {
+    // exactly one lane of the record holds it: OR over the 8 lanes
+    trl |= __shfl_xor(trl, 1);
+    trl |= __shfl_xor(trl, 2);
+    trl |= __shfl_xor(trl, 4);
+    if (have && l == 0) p.trailer[di] = (valid && ok) ? trl : 0u;
   }
   if (have && l == 0)
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
@@ -569,7 +590,10 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
       const uint32_t di = p.order ? p.order[pos] : pos;
       if (mode != ESPGPU_CSP_MODE_AEAD) {
         // no session: EINVAL; an ETA session's records belong to the ETA kernel
-        if (mode == 0 && have && (tid & 7) == 0) p.status[di] = ESPGPU_EINVAL;
+        if (mode == 0 && have && (tid & 7) == 0) {
+          p.status[di] = ESPGPU_EINVAL;
+          if (MODE != 1 && p.trailer) p.trailer[di] = 0;
+        }
         continue;
       }
       do_group<MODE, PAIR, KR>(p, lds, di, have, sa, flags, mlen, (int)nr,

@@ -192,7 +192,8 @@ void free_slot(Slot &s) {
 
 // Launch the crypto kernels for one batch of device-resident records.
 int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
-              uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st) {
+              uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st,
+              uint32_t *d_trailer = nullptr) {
   if (n == 0) return 0;
   const uint32_t nsas = (uint32_t)c->sessions.size();
   GcmParams p{};
@@ -206,6 +207,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   p.status = d_status;
   p.nsas = nsas;
   p.queue = c->d_queue;
+  p.trailer = encrypt ? nullptr : d_trailer;
   if (!(flags & ESPGPU_BATCH_GROUPED)) {
     int e = ensure_plan(c, n);
     if (e) return e;
@@ -227,6 +229,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.chunks = p.chunks;
     q.nchunks = p.nchunks;
     q.queue = c->d_queue + 2;
+    q.trailer = p.trailer;
     q.n = n;
     q.sas = c->d_sas;
     q.tpair = c->d_tpair;
@@ -626,6 +629,14 @@ int espgpu_decrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_d
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return EINVAL;
   return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
                    reinterpret_cast<hipStream_t>(stream));
+}
+
+int espgpu_decrypt_batch_trailer(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc,
+                                 uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t *d_trailer,
+                                 uint32_t flags, void *stream) {
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_trailer && n)) return EINVAL;
+  return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
+                   reinterpret_cast<hipStream_t>(stream), d_trailer);
 }
 
 int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,

@@ -67,6 +67,7 @@ struct GcmParams {
   // launch; the last workgroup to retire resets both, so no per-launch memset.
   // Launches sharing a ctx must be stream-ordered (as the planner workspace).
   uint32_t *queue;
+  uint32_t *trailer;              // decrypt: fused esp_input_cb trailer words, or nullptr
 };
 
 struct EtaParams {
@@ -77,6 +78,7 @@ struct EtaParams {
   const Chunk *chunks;            // ETA chunks are [nchunks[0], nchunks[1])
   const uint32_t *nchunks;
   uint32_t *queue;                // [0] ticket, [1] retired waves (self-resetting)
+  uint32_t *trailer;              // decrypt: fused esp_input_cb trailer words, or nullptr
   uint32_t n;
   const DevSA *sas;
   const uint2 *tpair;             // encryption pair table
@@ -85,6 +87,18 @@ struct EtaParams {
   uint8_t *status;
   uint32_t nsas;
 };
+
+// esp_input_cb's checks on the last 3 plaintext bytes (xform_esp.c:597-630),
+// given the 4-byte-aligned dword holding them (bytes 1..3 in memory order)
+// and the payload (ESP ciphertext) length.  Bits as ESPGPU_TR_* (espgpu.h).
+__host__ __device__ inline uint32_t esp_trailer_word(uint32_t wlast, uint32_t plen) {
+  const uint32_t l0 = (wlast >> 8) & 0xffu, padlen = (wlast >> 16) & 0xffu, nh = wlast >> 24;
+  uint32_t t = nh | (padlen << 8) | ESPGPU_TR_VALID;
+  if (padlen + 2 > plen) t |= ESPGPU_TR_BADLEN;
+  if (padlen != l0 && padlen != 0) t |= ESPGPU_TR_BADPAD;
+  if (nh == 59) t |= ESPGPU_TR_NONE;                       // IPPROTO_NONE
+  return t;
+}
 
 // Launchers (defined in the .hip files, called by espgpu.cpp).
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream);

@@ -28,6 +28,10 @@ CRYPTO_F_IV_SEPARATE = 0x0200
 CRYPTO_HINT_MORE = 0x1
 CRYPTODEV_PROBE_HARDWARE = -100
 BATCH_GROUPED = 0x1
+TR_BADLEN = 0x00010000
+TR_BADPAD = 0x00020000
+TR_NONE = 0x00040000
+TR_VALID = 0x80000000
 EINVAL = 22
 EBADMSG = 74
 ERESTART = 85
@@ -113,6 +117,7 @@ def lib():
         L.espgpu_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.espgpu_decrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint32, vp]
         L.espgpu_encrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp]
+        L.espgpu_decrypt_batch_trailer.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint32, vp]
         L.espgpu_last_kernel_ms.argtypes = [vp]
         L.espgpu_last_kernel_ms.restype = C.c_float
         L.espgpu_set_tuning.argtypes = [vp, C.c_char_p, C.c_int]

@@ -26,14 +26,25 @@ def _stream_ptr(stream):
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
 
 
-def decrypt_batch(driver, arena, desc, n, status, out=None, grouped=False, stream=None):
-    """Verify+decrypt n records.  out=None -> in place (verify-first two-pass)."""
-    for t in (arena, desc, status) + ((out,) if out is not None else ()):
+def decrypt_batch(driver, arena, desc, n, status, out=None, grouped=False, stream=None,
+                  trailer=None):
+    """Verify+decrypt n records.  out=None -> in place (verify-first two-pass).
+    trailer: optional int32/uint32 CUDA tensor of n words receiving the fused
+    esp_input_cb trailer checks (espgpu_decrypt_batch_trailer; see
+    esp.trailer_word for the bit layout)."""
+    for t in (arena, desc, status) + tuple(x for x in (out, trailer) if x is not None):
         assert t.is_cuda and t.is_contiguous()
-    rc = driver.lib.espgpu_decrypt_batch(
-        driver.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(),
-        out.data_ptr() if out is not None else None,
-        L.BATCH_GROUPED if grouped else 0, _stream_ptr(stream))
+    outp = out.data_ptr() if out is not None else None
+    flags = L.BATCH_GROUPED if grouped else 0
+    if trailer is not None:
+        assert trailer.numel() >= n and trailer.element_size() == 4
+        rc = driver.lib.espgpu_decrypt_batch_trailer(
+            driver.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(), outp,
+            trailer.data_ptr(), flags, _stream_ptr(stream))
+    else:
+        rc = driver.lib.espgpu_decrypt_batch(
+            driver.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(), outp, flags,
+            _stream_ptr(stream))
     if rc:
         raise RuntimeError("espgpu_decrypt_batch: %s" % driver.last_error())
 

@@ -130,6 +130,33 @@ def esp_pad(inner, blocksize=4, next_header=4):
     return bytes(inner) + pad
 
 
+def trailer_word(plain_payload):
+    """The 32-bit word the kernels' fused trailer check produces for a
+    decrypted payload (espgpu_decrypt_batch_trailer, include/espgpu.h):
+    next header | pad length << 8 | TR_* flags | TR_VALID."""
+    from . import _lib as L
+    p = bytes(plain_payload)
+    l0, padlen, nh = p[-3], p[-2], p[-1]
+    t = nh | (padlen << 8) | L.TR_VALID
+    if padlen + 2 > len(p):
+        t |= L.TR_BADLEN
+    if padlen != l0 and padlen != 0:
+        t |= L.TR_BADPAD
+    if nh == IPPROTO_NONE:
+        t |= L.TR_NONE
+    return t
+
+
+def trailer_accepts(word, prand=False):
+    """esp_input_cb's verdict (xform_esp.c:597-630) from a trailer word:
+    True = keep the packet.  prand: the SA uses random padding
+    (SADB_X_EXT_PRAND), which skips the pad-content check."""
+    from . import _lib as L
+    if not word & L.TR_VALID or word & (L.TR_BADLEN | L.TR_NONE):
+        return False
+    return prand or not word & L.TR_BADPAD
+
+
 def esp_trailer_ok(plain_payload):
     """The checks esp_input_cb makes on the last three plaintext bytes
     (xform_esp.c:597-630, default SADB_X_EXT_PSEQ padding)."""

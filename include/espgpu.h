@@ -177,6 +177,25 @@ int  espgpu_decrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu
 int  espgpu_encrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
                           uint32_t n, uint8_t *d_status, uint32_t flags, void *stream);
 
+/* Decrypt + the ESP trailer checks of esp_input_cb (xform_esp.c:597-630)
+ * fused into the kernels: d_trailer[i] (one 32-bit word per record) gets
+ *   bits 0-7  next header, bits 8-15 pad length (the last 3 plaintext bytes),
+ *   ESPGPU_TR_BADLEN  pad length + 2 > payload length       (esps_badilen),
+ *   ESPGPU_TR_BADPAD  last pad byte != pad length != 0       (esps_badenc; the
+ *                     caller ignores it for SADB_X_EXT_PRAND SAs),
+ *   ESPGPU_TR_NONE    next header == IPPROTO_NONE (59)       (silent drop),
+ *   ESPGPU_TR_VALID   set for every record whose status is 0;
+ * and 0 for records that failed (status != 0).  Otherwise as
+ * espgpu_decrypt_batch. */
+#define ESPGPU_TR_BADLEN 0x00010000u
+#define ESPGPU_TR_BADPAD 0x00020000u
+#define ESPGPU_TR_NONE   0x00040000u
+#define ESPGPU_TR_VALID  0x80000000u
+int  espgpu_decrypt_batch_trailer(espgpu_ctx *ctx, uint8_t *d_arena,
+                                  const struct espgpu_desc *d_desc, uint32_t n,
+                                  uint8_t *d_status, uint8_t *d_out, uint32_t *d_trailer,
+                                  uint32_t flags, void *stream);
+
 /* Host-to-host pipelined decrypt of a large host-resident batch (the shape of
  * an offload from DPDK hugepage mbufs): records in h_arena (pinned: hipHostMalloc
  * or hipHostRegister), descriptors in ascending arena order; `chunk` records per

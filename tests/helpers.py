@@ -39,11 +39,13 @@ class EtaSA:
                            flags=O.CSP_F_ESN if esn else 0)
 
 
-def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None):
+def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None, tails=None):
     """Plaintext ESP records + oracle-encrypted copies in one arena.
 
     Returns (arena_plain, arena_ct, descs, esn_hi) as numpy arrays; records are
     placed at 4-byte aligned offsets (stride_pad adds slack between records).
+    tails: {record index: 3 bytes} forced as the payload's last three bytes
+    (last pad byte, pad length, next header).
     """
     n = len(sa_idx)
     hlen = 16 if gcm else 24
@@ -66,6 +68,8 @@ def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None
         rec[0:4] = np.frombuffer(sa.spi.to_bytes(4, "big"), dtype=np.uint8)
         rec[4:8] = np.frombuffer(int(i + 1).to_bytes(4, "big"), dtype=np.uint8)
         rec[L - alen:] = 0
+        if tails is not None and i in tails:        # last 3 payload bytes
+            rec[L - alen - 3:L - alen] = np.frombuffer(bytes(tails[i]), dtype=np.uint8)
     descs = np.zeros(n, dtype=DESC)
     descs["off4"] = offs // 4
     descs["len"] = lens
