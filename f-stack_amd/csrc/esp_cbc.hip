@@ -374,6 +374,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         }
         const uint32_t ro = __shfl(off, j);
         const uint32_t rpl = __shfl(plen, j), rdi = __shfl(di, j);
+        const int rok = __shfl((int)ok, j);        // MODE 0 also decrypts failed records
         if (f >= 0) {
           const uint32_t i = (uint32_t)f - sj;
           const uint8_t *rec = p.arena + ro;
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           const uint4 prev = ld16(rec + 8 + 16 * i);         // C_{i-1}, or the IV for i = 0
           const uint4 pt = xor4(aes_dec(c, dk, nr, lds, slot), prev);
           st16(obase + ro + 24 + 16 * i, pt);
-          if (p.trailer && i == rpl / 16 - 1) p.trailer[rdi] = esp_trailer_word(pt.w, rpl);
+          if (p.trailer && i == rpl / 16 - 1 && rok) p.trailer[rdi] = esp_trailer_word(pt.w, rpl);
         }
       }
     }

@@ -44,6 +44,8 @@ namespace {
 // fit the DS instructions' 16-bit immediate), the AES T-table at 64 KiB.
 constexpr uint32_t LDS_GT = 0;          // H^8, 16 positions x 256 values x 16 B
 constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
+constexpr uint32_t PW8 = 0;             // 4-bit kernels: H^8 at 0, H^16 at 8 KiB
+constexpr uint32_t PW16 = kGhPowerBytes;
 constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
 constexpr int S = 8;                    // lanes per record
 
@@ -299,6 +301,80 @@ __device__ __forceinline__ uint4 gf_mul8(uint4 x, const uint8_t *lds) {
   return make_uint4(r0, r1, r2, r3);
 }
 
+// 4-bit variant (GH8 = false): H^8 and H^16 tables in LDS (8 KiB each).
+// pb = LDS byte address of the power's 8 KiB table (low byte 0, < 2^24).
+// Nibble position j = 8k + 2q (+1 for the high nibble) of word k, byte q.
+__device__ __forceinline__ uint4 gf_mul(uint4 x, uint32_t pb, const uint8_t *lds) {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  // One 32-bit word (8 nibble positions) per iteration; the loop is kept
+  // rolled so at most 8 lookups (32 VGPRs) are in flight per wave, and the
+  // word in use is rotated into w instead of indexing an array (which would
+  // go to scratch).  pb advances 8 position tables (2 KiB) per word.
+  uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t hi = w & 0xF0F0F0F0u;           // high nibble * 16, per byte
+    const uint32_t lo = (w << 4) & 0xF0F0F0F0u;    // low nibble * 16, per byte
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t sel = 0x0c060500u | (uint32_t)q;
+      const uint32_t alo = perm(pb, lo, sel);
+      const uint32_t ahi = perm(pb, hi, sel);
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + alo + (2 * q) * 256);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + ahi + (2 * q + 1) * 256);
+      r0 = xor3(r0, e.x, f.x);
+      r1 = xor3(r1, e.y, f.y);
+      r2 = xor3(r2, e.z, f.z);
+      r3 = xor3(r3, e.w, f.w);
+    }
+    w = w1;
+    w1 = w2;
+    w2 = w3;
+    pb += 8 * 256;
+  }
+  return make_uint4(r0, r1, r2, r3);
+}
+
+// Two independent products x * P and y * Q in one rolled word loop: 4 table
+// rows in flight per lookup group instead of 2.
+__device__ __forceinline__ void gf_mul2(uint4 x, uint32_t px, uint4 y, uint32_t py,
+                                        const uint8_t *lds, uint4 &rx, uint4 &ry) {
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+  uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
+  uint32_t v = y.x, v1 = y.y, v2 = y.z, v3 = y.w;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t hw = w & 0xF0F0F0F0u, lw = (w << 4) & 0xF0F0F0F0u;
+    const uint32_t hv = v & 0xF0F0F0F0u, lv = (v << 4) & 0xF0F0F0F0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t sel = 0x0c060500u | (uint32_t)q;
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + perm(px, lw, sel) + (2 * q) * 256);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + perm(px, hw, sel) + (2 * q + 1) * 256);
+      const uint4 g = *reinterpret_cast<const uint4 *>(lds + perm(py, lv, sel) + (2 * q) * 256);
+      const uint4 h = *reinterpret_cast<const uint4 *>(lds + perm(py, hv, sel) + (2 * q + 1) * 256);
+      a0 = xor3(a0, e.x, f.x);
+      a1 = xor3(a1, e.y, f.y);
+      a2 = xor3(a2, e.z, f.z);
+      a3 = xor3(a3, e.w, f.w);
+      b0 = xor3(b0, g.x, h.x);
+      b1 = xor3(b1, g.y, h.y);
+      b2 = xor3(b2, g.z, h.z);
+      b3 = xor3(b3, g.w, h.w);
+    }
+    w = w1;
+    w1 = w2;
+    w2 = w3;
+    v = v1;
+    v1 = v2;
+    v2 = v3;
+    px += 8 * 256;
+    py += 8 * 256;
+  }
+  rx = make_uint4(a0, a1, a2, a3);
+  ry = make_uint4(b0, b1, b2, b3);
+}
+
 // Y * H^e with the 4-bit table of that power in global memory (t = its 8 KiB:
 // nibble position j (byte j>>1, low nibble if j even), value n at j*256+n*16).
 // Used once per record per lane (the final x H^(8-l)), where the power differs
@@ -345,7 +421,7 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // PAIR: steps m, m+1 of a lane run together (2 independent AES blocks, and
 // Y <- Y*H^16 ^ B_m*H^8 ^ B_m+1 as 2 independent GHASH products); KR: the
 // pair's last KR AES rounds are bitsliced (0 = all T-table).
-template <int MODE, bool PAIR, int KR>
+template <int MODE, bool PAIR, int KR, bool GH8>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di,
                                                    bool have, uint32_t sa, uint32_t sa_flags,
                                                    uint32_t mlen, int nr, rkptr rk, rkptr bsk) {
@@ -439,12 +515,23 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         if (MODE != 2) aes_ctr2<KR>(cc, ca, cb, rk3, nr, rk, bsk, lds, slot, ka, kb);
         const uint4 Ba = block_in(i, hca, Ca, ka);
         const uint4 Bb = block_in(ib, hcb, Cb, kb);
-        const uint4 P = (gopts() & 2) ? Y : gf_mul8(Y, lds);
-        // M >= m+2: Y = (Y*H^8 ^ Ba)*H^8 ^ Bb;  M == m+1: Y = Y*H^8 ^ Ba
-        if (M >= m + 1) {
-          const uint4 Ym = xor4(P, Ba);
-          Y = Ym;
-          if (M >= m + 2) Y = xor4((gopts() & 2) ? Ym : gf_mul8(Ym, lds), Bb);
+        if (gopts() & 2) {
+        } else if (GH8) {
+          // M >= m+2: Y = (Y*H^8 ^ Ba)*H^8 ^ Bb;  M == m+1: Y = Y*H^8 ^ Ba
+          const uint4 P = gf_mul8(Y, lds);
+          if (M >= m + 1) {
+            const uint4 Ym = xor4(P, Ba);
+            Y = Ym;
+            if (M >= m + 2) Y = xor4(gf_mul8(Ym, lds), Bb);
+          }
+        } else {
+          // M >= m+2: Y = Y*H^16 ^ Ba*H^8 ^ Bb (two independent products);
+          // M == m+1: Y = Y*H^8 ^ Ba
+          const bool two = M >= m + 2;
+          uint4 P, Q;
+          gf_mul2(Y, two ? PW16 : PW8, Ba, PW8, lds, P, Q);
+          if (two) Y = xor4(xor4(P, Q), Bb);
+          else if (M == m + 1) Y = xor4(P, Ba);
         }
         m += 2;
         continue;
@@ -459,7 +546,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
     uint4 ks = make_uint4(0, 0, 0, 0);
     if (m > 0 && !(gopts() & 2)) {
-      const uint4 Yn = gf_mul8(Y, lds);
+      const uint4 Yn = GH8 ? gf_mul8(Y, lds) : gf_mul(Y, PW8, lds);
       if (m < M) Y = Yn;
     }
     if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
@@ -474,7 +561,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     ++m;
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
-  uint4 Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + kGh8Bytes +
+  uint4 Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + kGh4Off +
                                  (uint32_t)(7 - l) * kGhPowerBytes);
   Z = xor4(Z, shfl_xor4(Z, 1));
   Z = xor4(Z, shfl_xor4(Z, 2));
@@ -524,7 +611,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
-template <int MODE, int WG, bool PAIR, int KR>
+template <int MODE, int WG, bool PAIR, int KR, bool GH8>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
@@ -572,10 +659,19 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         flags = s->flags;
         mlen = s->mlen;
         mode = s->mode;
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes);
+        const uint8_t *tab = p.gtab + (size_t)sa * kGhTableBytes;
         uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
+        if (GH8) {
+          const uint4 *src = reinterpret_cast<const uint4 *>(tab);
 #pragma unroll 4
-        for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+          for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+        } else {
+          // 4-bit H^8 then H^16 (PW8, PW16)
+          const uint4 *s8 = reinterpret_cast<const uint4 *>(tab + kGh4Off + 7 * kGhPowerBytes);
+          const uint4 *s16 = reinterpret_cast<const uint4 *>(tab + kGh16Off);
+          constexpr int Q = (int)(kGhPowerBytes / 16);
+          for (int q = tid; q < 2 * Q; q += WG) dst[q] = q < Q ? s8[q] : s16[q - Q];
+        }
       } else {
         mode = 0;
       }
@@ -596,7 +692,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         continue;
       }
-      do_group<MODE, PAIR, KR>(p, lds, di, have, sa, flags, mlen, (int)nr,
+      do_group<MODE, PAIR, KR, GH8>(p, lds, di, have, sa, flags, mlen, (int)nr,
                                (rkptr)(const void *)(p.sas[sa].rk),
                                (rkptr)(const void *)(p.sas[sa].dk));
     }
@@ -613,28 +709,37 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
 
 // variant: bit0 = 512-thread workgroups (2 waves/SIMD, 256 VGPRs) instead of
 // 1024 (4 waves/SIMD, 128 VGPRs); bit1 = PAIR (two steps per lane at once);
-// bits 2-3 (PAIR, 1024 only) = bitsliced tail rounds KR = 0, 2, 3, 4.
+// bits 2-3 (PAIR, 1024 only) = bitsliced tail rounds KR = 0, 2, 3, 4;
+// bit 4 (1024 only) = GHASH with 4-bit LDS tables instead of 8-bit.
 template <int MODE>
 static void launch_mode(const GcmParams &p, int variant, int grid, hipStream_t st) {
   const int kr = (variant >> 2) & 3;
+  const bool gh4 = (variant >> 4) & 1;
+#define GCM_LAUNCH(WG, PR, KR, G8) \
+  hipLaunchKernelGGL((gcm_kernel<MODE, WG, PR, KR, G8>), dim3(grid), dim3(WG), 0, st, p)
   switch (variant & 3) {
-    case 0: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, false, 0>), dim3(grid), dim3(1024), 0, st, p); break;
-    case 1: hipLaunchKernelGGL((gcm_kernel<MODE, 512, false, 0>), dim3(grid), dim3(512), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((gcm_kernel<MODE, 512, true, 0>), dim3(grid), dim3(512), 0, st, p); break;
+    case 0: if (gh4) GCM_LAUNCH(1024, false, 0, false); else GCM_LAUNCH(1024, false, 0, true); break;
+    case 1: GCM_LAUNCH(512, false, 0, true); break;
+    case 3: GCM_LAUNCH(512, true, 0, true); break;
     default:
+      if (gh4) {
+        GCM_LAUNCH(1024, true, 0, false);
+        break;
+      }
       switch (kr) {
-        case 0: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 0>), dim3(grid), dim3(1024), 0, st, p); break;
-        case 1: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 2>), dim3(grid), dim3(1024), 0, st, p); break;
-        case 2: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 3>), dim3(grid), dim3(1024), 0, st, p); break;
-        default: hipLaunchKernelGGL((gcm_kernel<MODE, 1024, true, 4>), dim3(grid), dim3(1024), 0, st, p); break;
+        case 0: GCM_LAUNCH(1024, true, 0, true); break;
+        case 1: GCM_LAUNCH(1024, true, 2, true); break;
+        case 2: GCM_LAUNCH(1024, true, 3, true); break;
+        default: GCM_LAUNCH(1024, true, 4, true); break;
       }
   }
+#undef GCM_LAUNCH
 }
 
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int variant, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   static int cur_opts = -1;
-  const uint32_t opts = (uint32_t)variant >> 4;
+  const uint32_t opts = (uint32_t)variant >> 5;
   if ((int)opts != cur_opts) {
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_opts), &opts, 4, 0, hipMemcpyHostToDevice, st);
     hipStreamSynchronize(st);

@@ -12,7 +12,7 @@ namespace espgpu {
 //   round (see esp_gcm.hip):  rk[0..3] raw, rk[4r..4r+3] = ror16(rk) for the
 //   middle rounds, rk[4nr..] byte-swapped (the last round emits little-endian
 //   words); dk[0..31] = bitsliced plane keys of the last 4 rounds (bsaes.h).
-//   The GHASH tables live in a separate 128 KiB-per-slot array.
+//   The GHASH tables live in a separate 136 KiB-per-slot array.
 // ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
 //   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
 //   = SHA-1 chaining state after one block of key^0x36 / key^0x5c
@@ -31,13 +31,18 @@ struct DevSA {
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 
 // GHASH multiplication tables for one SA (host_crypto.cpp ghash_tables):
-// [0, 64 KiB) H^8 with 8-bit indices, entry (byte position p, value v) at
-// p*4096 + v*16 -- staged in LDS for the per-block Horner multiply;
-// [64 KiB, 128 KiB) H^1..H^8 with 4-bit indices (8 KiB per power) -- read
-// from global memory (L2) by the once-per-record final multiply.
+// [0, 64 KiB)          H^8 with 8-bit indices, entry (byte position p, value
+//                      v) at p*4096 + v*16 (LDS, GH8 kernels);
+// [kGh4Off, +64 KiB)   H^1..H^8 with 4-bit indices, 8 KiB per power: nibble
+//                      position j (byte j>>1, low nibble if j even), value n
+//                      at j*256 + n*16 (H^8 in LDS for 4-bit kernels; all of
+//                      them from global memory for the per-record final);
+// [kGh16Off, +8 KiB)   H^16 with 4-bit indices (LDS, 4-bit paired kernels).
 constexpr uint32_t kGh8Bytes = 16 * 256 * 16;                    // 65536
 constexpr uint32_t kGhPowerBytes = 32 * 16 * 16;                 // 8192
-constexpr uint32_t kGhTableBytes = kGh8Bytes + 8 * kGhPowerBytes;  // 131072
+constexpr uint32_t kGh4Off = kGh8Bytes;
+constexpr uint32_t kGh16Off = kGh4Off + 8 * kGhPowerBytes;
+constexpr uint32_t kGhTableBytes = kGh16Off + kGhPowerBytes;     // 139264
 
 // A chunk: up to kChunkRecs records of ONE session, processed by one
 // workgroup iteration of the GCM kernel.  rec positions index `order`

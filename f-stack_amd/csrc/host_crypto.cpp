@@ -154,9 +154,9 @@ void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
 void ghash_tables(const uint8_t h[16], uint8_t *out) {
   // Section 1 (kGh8Bytes): H^8 with 8-bit indices: entry (p, v) at p*4096 +
   //   v*16 = (the block whose byte p is v, all else 0) * H^8.
-  // Section 2 (kGh4Bytes, at kGh8Bytes): powers H^1..H^8 (index 0..7) with
-  //   4-bit indices: power p, nibble position j (byte j>>1, low nibble if j
-  //   even), value n at p*8192 + j*256 + n*16.
+  // Section 2 (at 65536): powers H^1..H^8 (index 0..7) with 4-bit indices:
+  //   power p, nibble position j (byte j>>1, low nibble if j even), value n
+  //   at p*8192 + j*256 + n*16.
   uint8_t pw[8][16];
   memcpy(pw[0], h, 16);
   for (int p = 1; p < 8; ++p) gf128_mul(pw[p - 1], h, pw[p]);
@@ -177,6 +177,27 @@ void ghash_tables(const uint8_t h[16], uint8_t *out) {
           if (n & (1 << t))
             for (int k = 0; k < 16; ++k) acc[k] ^= bit[byte * 8 + sh + t][k];
         memcpy(t4 + ((size_t)p * 32 * 16 + (size_t)j * 16 + n) * 16, acc, 16);
+      }
+    }
+  }
+  // Section 3 (at 65536 + 8*8192): H^16 with 4-bit indices
+  {
+    uint8_t h16[16], bit[128][16];
+    gf128_mul(pw[7], pw[7], h16);
+    for (int b = 0; b < 128; ++b) {
+      uint8_t e[16] = {0};
+      e[b >> 3] = (uint8_t)(1u << (b & 7));
+      gf128_mul(e, h16, bit[b]);
+    }
+    uint8_t *t16 = out + 65536 + 8 * 8192;
+    for (int j = 0; j < 32; ++j) {
+      const int byte = j >> 1, sh = (j & 1) * 4;
+      for (int n = 0; n < 16; ++n) {
+        uint8_t acc[16] = {0};
+        for (int t = 0; t < 4; ++t)
+          if (n & (1 << t))
+            for (int k = 0; k < 16; ++k) acc[k] ^= bit[byte * 8 + sh + t][k];
+        memcpy(t16 + (size_t)j * 256 + n * 16, acc, 16);
       }
     }
   }

@@ -341,7 +341,7 @@ def test_host_pipeline_vs_oracle(drv, chunk):
         drv.freesession(s)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 10, 14])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 10, 14, 16, 18])
 def test_kernel_variants_vs_oracle(drv, variant):
     """Every GCM kernel variant (workgroup size x paired steps x bitsliced
     tail rounds) decrypts,

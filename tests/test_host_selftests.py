@@ -30,7 +30,9 @@ def test_ghash_table_layout_selftest(tmp_path):
     # the self-test mirrors these constants; keep them in step with the header
     assert re.search(r"kGh8Bytes = 16 \* 256 \* 16;", hdr)
     assert re.search(r"kGhPowerBytes = 32 \* 16 \* 16;", hdr)
-    assert re.search(r"kGhTableBytes = kGh8Bytes \+ 8 \* kGhPowerBytes;", hdr)
+    assert re.search(r"kGh4Off = kGh8Bytes;", hdr)
+    assert re.search(r"kGh16Off = kGh4Off \+ 8 \* kGhPowerBytes;", hdr)
+    assert re.search(r"kGhTableBytes = kGh16Off \+ kGhPowerBytes;", hdr)
     exe = tmp_path / "ghash_selftest"
     csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),

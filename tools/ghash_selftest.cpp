@@ -10,11 +10,12 @@
 #include <vector>
 
 // layout constants, mirrored from espgpu_internal.h (which needs HIP vector types)
-static constexpr unsigned kGh8Bytes = 65536, kGhPowerBytes = 8192, kGhTableBytes = 131072;
+static constexpr unsigned kGh8Bytes = 65536, kGhPowerBytes = 8192, kGh4Off = 65536,
+                          kGh16Off = 65536 + 8 * 8192, kGhTableBytes = 139264;
 #include "host_crypto.h"
 
 using namespace espgpu;
-static_assert(kGhTableBytes == kGh8Bytes + 8 * kGhPowerBytes, "layout");
+static_assert(kGhTableBytes == kGh16Off + kGhPowerBytes, "layout");
 
 static void xor16(uint8_t *a, const uint8_t *b) { for (int i = 0; i < 16; ++i) a[i] ^= b[i]; }
 
@@ -49,9 +50,14 @@ int main() {
       if (memcmp(a, b, 16)) { printf("8-bit H^8 table mismatch\n"); return 1; }
       for (int e = 1; e <= 8; ++e) {
         hc::gf128_mul(x, pw[e], a);
-        mul4(tabs.data() + kGh8Bytes + (e - 1) * kGhPowerBytes, x, b);
+        mul4(tabs.data() + kGh4Off + (e - 1) * kGhPowerBytes, x, b);
         if (memcmp(a, b, 16)) { printf("4-bit H^%d table mismatch\n", e); return 1; }
       }
+      uint8_t h16[16];
+      hc::gf128_mul(pw[8], pw[8], h16);
+      hc::gf128_mul(x, h16, a);
+      mul4(tabs.data() + kGh16Off, x, b);
+      if (memcmp(a, b, 16)) { printf("4-bit H^16 table mismatch\n"); return 1; }
     }
     // stride-8 Horner over N blocks (front-padded to 8M) vs serial GHASH
     for (int N : {1, 3, 8, 9, 93, 562}) {
@@ -68,7 +74,7 @@ int main() {
           const int i = 8 * m + l - pad;
           if (i >= 0) xor16(Y, &X[16 * i]);
         }
-        mul4(tabs.data() + kGh8Bytes + (7 - l) * kGhPowerBytes, Y, t);
+        mul4(tabs.data() + kGh4Off + (7 - l) * kGhPowerBytes, Y, t);
         xor16(Z, t);
       }
       if (memcmp(Z, ser, 16)) { printf("Horner mismatch N=%d\n", N); return 1; }
