@@ -418,9 +418,10 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
-// PAIR: steps m, m+1 of a lane run together (2 independent AES blocks, and
-// Y <- Y*H^16 ^ B_m*H^8 ^ B_m+1 as 2 independent GHASH products); KR: the
-// pair's last KR AES rounds are bitsliced (0 = all T-table).
+// PAIR: steps m, m+1 of a lane run together: 2 independent AES blocks, then
+// GHASH either as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with 8-bit tables (GH8) or as
+// Y*H^16 ^ B_m*H^8 ^ B_m+1, 2 independent 4-bit products; KR: the pair's
+// last KR AES rounds are bitsliced (0 = all T-table).
 template <int MODE, bool PAIR, int KR, bool GH8>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di,
                                                    bool have, uint32_t sa, uint32_t sa_flags,
