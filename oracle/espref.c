@@ -193,47 +193,52 @@ int oref_aes_setkey_dec(uint32_t rk[60], const uint8_t *key, int keybits)
 /* rijndaelEncrypt, rijndael-alg-fst.c:863-1042 */
 void oref_aes_encrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16])
 {
-	uint32_t s[4], t[4];
+	/* scalar state words as rijndaelEncrypt keeps them (s0..s3 / t0..t3) */
+	uint32_t s0 = ld_be32(in) ^ rk[0], s1 = ld_be32(in + 4) ^ rk[1];
+	uint32_t s2 = ld_be32(in + 8) ^ rk[2], s3 = ld_be32(in + 12) ^ rk[3];
+	uint32_t t0, t1, t2, t3;
 
-	for (int c = 0; c < 4; c++)
-		s[c] = ld_be32(in + 4 * c) ^ rk[c];
 	for (int r = 1; r < nr; r++) {
-		for (int c = 0; c < 4; c++)
-			t[c] = TE[0][s[c] >> 24] ^ TE[1][(s[(c + 1) & 3] >> 16) & 0xff] ^
-			    TE[2][(s[(c + 2) & 3] >> 8) & 0xff] ^ TE[3][s[(c + 3) & 3] & 0xff] ^
-			    rk[4 * r + c];
-		memcpy(s, t, sizeof(s));
+		rk += 4;
+		t0 = TE[0][s0 >> 24] ^ TE[1][(s1 >> 16) & 0xff] ^ TE[2][(s2 >> 8) & 0xff] ^ TE[3][s3 & 0xff] ^ rk[0];
+		t1 = TE[0][s1 >> 24] ^ TE[1][(s2 >> 16) & 0xff] ^ TE[2][(s3 >> 8) & 0xff] ^ TE[3][s0 & 0xff] ^ rk[1];
+		t2 = TE[0][s2 >> 24] ^ TE[1][(s3 >> 16) & 0xff] ^ TE[2][(s0 >> 8) & 0xff] ^ TE[3][s1 & 0xff] ^ rk[2];
+		t3 = TE[0][s3 >> 24] ^ TE[1][(s0 >> 16) & 0xff] ^ TE[2][(s1 >> 8) & 0xff] ^ TE[3][s2 & 0xff] ^ rk[3];
+		s0 = t0; s1 = t1; s2 = t2; s3 = t3;
 	}
-	for (int c = 0; c < 4; c++) {
-		uint32_t v = ((uint32_t)SBOX[s[c] >> 24] << 24) |
-		    ((uint32_t)SBOX[(s[(c + 1) & 3] >> 16) & 0xff] << 16) |
-		    ((uint32_t)SBOX[(s[(c + 2) & 3] >> 8) & 0xff] << 8) |
-		    SBOX[s[(c + 3) & 3] & 0xff];
-		st_be32(out + 4 * c, v ^ rk[4 * nr + c]);
-	}
+	rk += 4;
+#define SB4(a, b, c, d) (((uint32_t)SBOX[(a) >> 24] << 24) | ((uint32_t)SBOX[((b) >> 16) & 0xff] << 16) | \
+	((uint32_t)SBOX[((c) >> 8) & 0xff] << 8) | SBOX[(d) & 0xff])
+	st_be32(out, SB4(s0, s1, s2, s3) ^ rk[0]);
+	st_be32(out + 4, SB4(s1, s2, s3, s0) ^ rk[1]);
+	st_be32(out + 8, SB4(s2, s3, s0, s1) ^ rk[2]);
+	st_be32(out + 12, SB4(s3, s0, s1, s2) ^ rk[3]);
+#undef SB4
 }
 
 /* rijndaelDecrypt, rijndael-alg-fst.c:1044-1222 (equivalent inverse cipher) */
 void oref_aes_decrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16])
 {
-	uint32_t s[4], t[4];
+	uint32_t s0 = ld_be32(in) ^ rk[0], s1 = ld_be32(in + 4) ^ rk[1];
+	uint32_t s2 = ld_be32(in + 8) ^ rk[2], s3 = ld_be32(in + 12) ^ rk[3];
+	uint32_t t0, t1, t2, t3;
 
-	for (int c = 0; c < 4; c++)
-		s[c] = ld_be32(in + 4 * c) ^ rk[c];
 	for (int r = 1; r < nr; r++) {
-		for (int c = 0; c < 4; c++)
-			t[c] = TD[0][s[c] >> 24] ^ TD[1][(s[(c + 3) & 3] >> 16) & 0xff] ^
-			    TD[2][(s[(c + 2) & 3] >> 8) & 0xff] ^ TD[3][s[(c + 1) & 3] & 0xff] ^
-			    rk[4 * r + c];
-		memcpy(s, t, sizeof(s));
+		rk += 4;
+		t0 = TD[0][s0 >> 24] ^ TD[1][(s3 >> 16) & 0xff] ^ TD[2][(s2 >> 8) & 0xff] ^ TD[3][s1 & 0xff] ^ rk[0];
+		t1 = TD[0][s1 >> 24] ^ TD[1][(s0 >> 16) & 0xff] ^ TD[2][(s3 >> 8) & 0xff] ^ TD[3][s2 & 0xff] ^ rk[1];
+		t2 = TD[0][s2 >> 24] ^ TD[1][(s1 >> 16) & 0xff] ^ TD[2][(s0 >> 8) & 0xff] ^ TD[3][s3 & 0xff] ^ rk[2];
+		t3 = TD[0][s3 >> 24] ^ TD[1][(s2 >> 16) & 0xff] ^ TD[2][(s1 >> 8) & 0xff] ^ TD[3][s0 & 0xff] ^ rk[3];
+		s0 = t0; s1 = t1; s2 = t2; s3 = t3;
 	}
-	for (int c = 0; c < 4; c++) {
-		uint32_t v = ((uint32_t)ISBOX[s[c] >> 24] << 24) |
-		    ((uint32_t)ISBOX[(s[(c + 3) & 3] >> 16) & 0xff] << 16) |
-		    ((uint32_t)ISBOX[(s[(c + 2) & 3] >> 8) & 0xff] << 8) |
-		    ISBOX[s[(c + 1) & 3] & 0xff];
-		st_be32(out + 4 * c, v ^ rk[4 * nr + c]);
-	}
+	rk += 4;
+#define ISB4(a, b, c, d) (((uint32_t)ISBOX[(a) >> 24] << 24) | ((uint32_t)ISBOX[((b) >> 16) & 0xff] << 16) | \
+	((uint32_t)ISBOX[((c) >> 8) & 0xff] << 8) | ISBOX[(d) & 0xff])
+	st_be32(out, ISB4(s0, s3, s2, s1) ^ rk[0]);
+	st_be32(out + 4, ISB4(s1, s0, s3, s2) ^ rk[1]);
+	st_be32(out + 8, ISB4(s2, s1, s0, s3) ^ rk[2]);
+	st_be32(out + 12, ISB4(s3, s2, s1, s0) ^ rk[3]);
+#undef ISB4
 }
 
 /* ------------------------------------------------------------------------ */

@@ -10,6 +10,7 @@
   reference tree is absent, e.g. on the GPU box).
 """
 import hashlib
+import os
 import hmac
 
 import numpy as np
@@ -134,3 +135,22 @@ def test_oracle_batch_roundtrip(gcm):
             assert st[i] == 0
             h = 16 if gcm else 24
             assert (out[o + h:o + L - alen] == plain[o + h:o + L - alen]).all()
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/freebsd"),
+                    reason="reference sources absent (GPU box): calibration runs where they are")
+def test_oracle_matches_reference_primitives_composed_as_swcr_gcm():
+    """oracle/calib_ref.c: the reference's own rijndaelEncrypt + gf128_mul
+    (compiled from /root/reference) composed in swcr_gcm's order decrypt the
+    same records to the same bytes and statuses as espref.c, and the per-record
+    time of the restatement (bench.py's cpu_baseline) is within 15 % of it."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "calib"], check=True, timeout=300)
+    r = subprocess.run([os.path.join(root, "oracle", "_ref", "calib_ref"), "4096"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["outputs_identical"] and res["tag_failures"] > 0
+    assert 0.85 < res["ratio_oracle_over_ref"] < 1.15, res
