@@ -53,6 +53,35 @@ def aggregate(dist, world, dt, nbytes, device):
     return float(t.item()), int(b.item())
 
 
+def per_rank(dist, world, rank, value, device):
+    """[value of rank 0, ..., value of rank world-1] (one all_reduce)."""
+    if world == 1:
+        return [value]
+    import torch
+    t = torch.zeros(world, dtype=torch.float64, device=device)
+    t[rank] = float(value)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]
+
+
+def hbm_copy_gbs(arena, reps=5):
+    """Measured device-to-device copy rate over the same arena (bytes read +
+    written / time): the practical HBM ceiling beside the 8 TB/s spec peak."""
+    import torch
+    dst = torch.empty_like(arena)
+    dst.copy_(arena)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(arena)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del dst
+    return 2 * arena.numel() / (ms * 1e-3) / 1e9
+
+
 def plan_packets(cfg, rank, world, rng):
     """(spis, sa_of_packet, sizes) of the records this rank processes.
 
@@ -211,6 +240,14 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_ms": round(kern_ms, 4)},
     }
+    try:
+        copy = hbm_copy_gbs(arena)
+        result["roofline"]["hbm_copy_gbs"] = round(copy, 1)
+        result["roofline"]["frac_of_copy"] = round(achieved / copy, 4)
+    except Exception as e:                       # informational only
+        log("hbm copy measurement skipped: %s" % e)
+    if world > 1:
+        result["config"]["packets_per_rank"] = per_rank(dist, world, rank, n, dev)
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(pmc):
         with open(pmc) as f:

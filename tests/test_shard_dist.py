@@ -80,6 +80,8 @@ def _rank_main(rank, world, port, q):
         mdt, total = bench.aggregate(dist, world, dt, nbytes, torch.device("cpu"))
         got = [None] * world
         dist.all_gather_object(got, (sorted(spis), len(sizes)))
+        counts = bench.per_rank(dist, world, rank, len(sizes), torch.device("cpu"))
+        assert counts == [g[1] for g in got]
         q.put((rank, mdt, total, nbytes, got))
     finally:
         dist.destroy_process_group()
