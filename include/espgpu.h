@@ -147,7 +147,9 @@ void espgpu_freesession(espgpu_ctx *ctx, int32_t session);
 /* CRYPTODEV_PROCESS (cryptodev_if.m:143-147): never blocks.  Stages the
  * request; returns 0, or ERESTART when the staging batch is full (the framework
  * then sets cc_qblocked and requeues, crypto.c:1451-1459).  Malformed requests
- * complete with crp_etype = EINVAL via poll(), as crypto_done would. */
+ * complete with crp_etype = EINVAL via poll(), as crypto_done would.  `hint`
+ * (CRYPTO_HINT_MORE) is accepted and ignored: staged requests launch at
+ * espgpu_flush (once per RX burst) or when a staging slot fills. */
 int  espgpu_process(espgpu_ctx *ctx, const struct espgpu_req *req, int hint);
 /* Launch everything staged so far: H2D, kernels and D2H on three ctx streams
  * chained by events, so consecutive batches overlap copies with kernels.
