@@ -1,0 +1,86 @@
+/*
+ * ff_gpucrypto_host.c — host-domain half of the F-Stack binding (INTEGRATION.md
+ * section 2).  It would live in lib/ as an FF_HOST_SRCS file: libc/HIP
+ * headers only, no FreeBSD kernel headers.  The kernel-domain driver
+ * (lib/ff_gpucrypto.c) converts struct cryptop /
+ * crypto_session_params into the espgpu_* mirrors and calls these entry
+ * points; ff_gpucrypto_poll() runs once per main_loop iteration
+ * (lib/ff_dpdk_if.c:2363) and hands completions back through
+ * ff_gpucrypto_done() (kernel domain, listed in lib/ff_api.symlist).
+ *
+ * Built here against include/espgpu.h and f-stack_amd/libespgpu.so by
+ * `make -C integration` (tests/test_integration.py), so the binding a
+ * maintainer adds is compile- and link-checked.
+ */
+#include <errno.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "espgpu.h"
+
+/* kernel-domain callbacks (weak so this file links standalone for tests) */
+void ff_gpucrypto_done(void *opaque, int etype) __attribute__((weak));
+void ff_gpucrypto_unblock(void) __attribute__((weak));
+
+static espgpu_ctx *g_ctx;          /* one F-Stack process = one lcore = one ctx */
+
+int ff_gpucrypto_host_init(int gpu)
+{
+	struct espgpu_config c = { 0 };
+
+	c.device = gpu;
+	return espgpu_init(&c, &g_ctx);
+}
+
+void ff_gpucrypto_host_fini(void)
+{
+	if (g_ctx) {
+		espgpu_drain(g_ctx);
+		espgpu_fini(g_ctx);
+		g_ctx = NULL;
+	}
+}
+
+/* CRYPTODEV_PROBESESSION: -100 (CRYPTODEV_PROBE_HARDWARE) or EINVAL.
+ * Host-only, valid before ff_gpucrypto_host_init. */
+int ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
+{
+	return espgpu_probesession(csp);
+}
+
+int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid)
+{
+	return g_ctx ? espgpu_newsession(g_ctx, csp, sid) : ENXIO;
+}
+
+void ff_gpucrypto_host_freesession(int32_t sid)
+{
+	if (g_ctx)
+		espgpu_freesession(g_ctx, sid);
+}
+
+/* CRYPTODEV_PROCESS: 0 or ERESTART (the framework requeues) */
+int ff_gpucrypto_host_process(const struct espgpu_req *r, int hint)
+{
+	return g_ctx ? espgpu_process(g_ctx, r, hint) : ENXIO;
+}
+
+/* main_loop hook: launch the burst's staged records, deliver completions */
+int ff_gpucrypto_poll(void)
+{
+	struct espgpu_completion c[256];
+	int n, i, total = 0, blocked;
+
+	if (!g_ctx)
+		return 0;
+	blocked = espgpu_flush(g_ctx);
+	while ((n = espgpu_poll(g_ctx, c, 256)) > 0) {
+		for (i = 0; i < n; i++)
+			if (ff_gpucrypto_done)
+				ff_gpucrypto_done(c[i].opaque, c[i].etype);
+		total += n;
+	}
+	if (total && ff_gpucrypto_unblock)
+		ff_gpucrypto_unblock();     /* crypto_unblock(id, CRYPTO_SYMQ), crypto.c:1191 */
+	return blocked ? -blocked : total;
+}
