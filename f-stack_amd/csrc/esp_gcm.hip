@@ -14,11 +14,12 @@
 //    multiplier H^8 over blocks l, l+8, l+16, ... of its record (the block list
 //    is front-padded with zero blocks to a multiple of 8, which leaves the hash
 //    unchanged), then multiplies by H^(8-l) and the 8 partials are XOR-reduced
-//    across the lane group.  Multiplication by a fixed H^e uses 4-bit tables
-//    indexed per nibble POSITION (32 x 16 x 16 B per power, in LDS), so there
-//    is no shift/reduce step: X*H^e = XOR_j T_e[j][nib_j(X)].  Each 256-byte
-//    position table spans all 64 LDS banks once, so a ds_read_b128 lookup is
-//    bank-conflict-free whatever the nibble values.
+//    across the lane group.  Multiplication by a fixed H^e uses tables indexed
+//    per byte or nibble POSITION, so there is no shift/reduce step:
+//    X*H^e = XOR_j T_e[j][digit_j(X)].  The Horner multiplier H^8 is in LDS,
+//    either with 8-bit indices (16 lookups; GH8, the default) or 4-bit
+//    indices (32 lookups, conflict-free: a 256-byte position table spans the
+//    64 banks once); the per-lane final H^(8-l) is gathered from L2.
 //  * AES-CTR uses T-tables Te0 and Te1 replicated 32x in LDS (entry x at x*256:
 //    Te0 in lane slots (lane&31)*4, Te1 128 bytes later): ds_read_b32 with every
 //    lane of a 32-lane group on its own bank -> conflict-free; the LDS address
