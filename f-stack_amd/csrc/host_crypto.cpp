@@ -152,17 +152,15 @@ void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
 }
 
 void ghash_tables(const uint8_t h[16], uint8_t *out) {
-  // Section 1 (kGh8Bytes): H^8 with 8-bit indices: entry (p, v) at p*4096 +
-  //   v*16 = (the block whose byte p is v, all else 0) * H^8.
-  // Section 2 (at 65536): powers H^1..H^8 (index 0..7) with 4-bit indices:
-  //   power p, nibble position j (byte j>>1, low nibble if j even), value n
-  //   at p*8192 + j*256 + n*16.
-  uint8_t pw[8][16];
+  // Powers H^1..H^8 (index 0..7), then H^16, each with 4-bit indices: power
+  // table p, nibble position j (byte j>>1, low nibble if j even), value n at
+  // p*8192 + j*256 + n*16 = (the block whose nibble j is n, all else 0) * H^e.
+  uint8_t pw[9][16];
   memcpy(pw[0], h, 16);
   for (int p = 1; p < 8; ++p) gf128_mul(pw[p - 1], h, pw[p]);
-  uint8_t *t4 = out + 65536;
-  for (int p = 0; p < 8; ++p) {
-    // products of every single-bit block with H^(p+1)
+  gf128_mul(pw[7], pw[7], pw[8]);                      // H^16
+  for (int p = 0; p < 9; ++p) {
+    // products of every single-bit block with the power
     uint8_t bit[128][16];
     for (int b = 0; b < 128; ++b) {
       uint8_t e[16] = {0};
@@ -176,39 +174,10 @@ void ghash_tables(const uint8_t h[16], uint8_t *out) {
         for (int t = 0; t < 4; ++t)
           if (n & (1 << t))
             for (int k = 0; k < 16; ++k) acc[k] ^= bit[byte * 8 + sh + t][k];
-        memcpy(t4 + ((size_t)p * 32 * 16 + (size_t)j * 16 + n) * 16, acc, 16);
+        memcpy(out + ((size_t)p * 32 * 16 + (size_t)j * 16 + n) * 16, acc, 16);
       }
     }
   }
-  // Section 3 (at 65536 + 8*8192): H^16 with 4-bit indices
-  {
-    uint8_t h16[16], bit[128][16];
-    gf128_mul(pw[7], pw[7], h16);
-    for (int b = 0; b < 128; ++b) {
-      uint8_t e[16] = {0};
-      e[b >> 3] = (uint8_t)(1u << (b & 7));
-      gf128_mul(e, h16, bit[b]);
-    }
-    uint8_t *t16 = out + 65536 + 8 * 8192;
-    for (int j = 0; j < 32; ++j) {
-      const int byte = j >> 1, sh = (j & 1) * 4;
-      for (int n = 0; n < 16; ++n) {
-        uint8_t acc[16] = {0};
-        for (int t = 0; t < 4; ++t)
-          if (n & (1 << t))
-            for (int k = 0; k < 16; ++k) acc[k] ^= bit[byte * 8 + sh + t][k];
-        memcpy(t16 + (size_t)j * 256 + n * 16, acc, 16);
-      }
-    }
-  }
-  // 8-bit H^8 table from the 4-bit H^8 one (GF(2)-linear in the block)
-  const uint8_t *h8 = t4 + (size_t)7 * 8192;
-  for (int p = 0; p < 16; ++p)
-    for (int v = 0; v < 256; ++v) {
-      const uint8_t *lo = h8 + (2 * p) * 256 + (v & 15) * 16;
-      const uint8_t *hi = h8 + (2 * p + 1) * 256 + (v >> 4) * 16;
-      for (int k = 0; k < 16; ++k) out[(size_t)p * 4096 + (size_t)v * 16 + k] = lo[k] ^ hi[k];
-    }
 }
 
 void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {

@@ -24,9 +24,8 @@ void aes_encrypt_block(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t
 // GF(2^128) product in GCM bit order (SP 800-38D Algorithm 1).
 void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
 
-// GHASH table set for the GCM kernel (kGhTableBytes, espgpu_internal.h): H^8
-// with 8-bit indices (64 KiB), H^1..H^8 with 4-bit indices (64 KiB), H^16
-// with 4-bit indices (8 KiB).
+// GHASH table set for the GCM kernel (kGhTableBytes, espgpu_internal.h):
+// H^1..H^8 then H^16, 8 KiB each, with 4-bit indices.
 void ghash_tables(const uint8_t h[16], uint8_t *out);
 
 // SHA-1 compression of one 64-byte block into state h[5].

@@ -1,5 +1,5 @@
 // plan.hip — device-side batch planner: groups ESP records by (size class,
-// session) so that each 128-record chunk of the GCM kernel has ONE session
+// session) so that each 256-record chunk of the GCM kernel has ONE session
 // (its GHASH power tables and round keys are staged once in LDS) and records
 // of similar length share a wave.  Three small kernels, no host round trip:
 //   plan_count   per-workgroup LDS histogram of keys, flushed with one global
@@ -11,7 +11,7 @@
 // Keys: [0, 4*nsas) = GCM records (class-major, largest class first),
 // 4*nsas = records with no valid session (chunked with sa = ~0 so the GCM
 // kernel marks them EINVAL), 4*nsas+1+s = records of ETA session s.  GCM and
-// invalid keys make 128-record chunks, ETA keys 64-record (one wave) chunks;
+// invalid keys make 256-record (kChunkRecs) chunks, ETA keys 64-record (one wave) chunks;
 // chunks are emitted in key order, so nchunks[0] = the GCM kernel's share and
 // [nchunks[0], nchunks[1]) the ETA kernel's.  Cost: two passes over the
 // 16-byte descriptors.

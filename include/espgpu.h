@@ -212,11 +212,8 @@ int  espgpu_decrypt_host(espgpu_ctx *ctx, const uint8_t *h_arena, uint64_t arena
  * batch stream), for the roofline accounting in bench.py. */
 float espgpu_last_kernel_ms(espgpu_ctx *ctx);
 
-/* Tuning knobs (engine-internal, for A/B measurement): "gcm_variant"
- * (bit0: 512-thread workgroups, bit1: paired steps -- two AES blocks and two
- * GHASH products in flight per lane; default 2; bits 3-4 are measurement-only
- * knobs that skip work and break results), "grid" (workgroups per launch,
- * 0 = 256).  Returns 0 or ENOENT. */
+/* Tuning knob (engine-internal, for A/B measurement): "grid" (workgroups
+ * per launch, 0 = 256, one per CU).  Returns 0 or ENOENT. */
 int  espgpu_set_tuning(espgpu_ctx *ctx, const char *key, int value);
 
 #ifdef __cplusplus
