@@ -86,8 +86,6 @@ struct espgpu_ctx {
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
   int n_eta = 0;
-  int gcm_sched = 0;          // GCM kernel schedule variant (esp_gcm.hip phases)
-  int n_gcm_nr[3] = {0, 0, 0};   // GCM sessions per key size (10/12/14 rounds)
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -219,10 +217,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  uint32_t nr_mask = 1;
-  for (int k = 1; k < 3; ++k)
-    if (c->n_gcm_nr[k] > 0) nr_mask |= 1u << k;
-  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, nr_mask, c->gcm_sched, st)) return fail(c, EIO, "GCM kernel launch failed");
+  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st)) return fail(c, EIO, "GCM kernel launch failed");
   if (c->n_eta > 0) {
     EtaParams q{};
     q.arena = d_arena;
@@ -265,7 +260,6 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
   if (!cfg.nbatches) cfg.nbatches = 2;
   c->cfg = cfg;
   c->device = cfg.device;
-  if (const char *v = getenv("ESPGPU_GCM_SCHED")) c->gcm_sched = atoi(v);
   int rc = 0;
   do {
     int ndev = 0;
@@ -394,14 +388,14 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   sa.flags = (uint32_t)csp->csp_flags;
   if (csp->csp_mode == ESPGPU_CSP_MODE_AEAD) {
     sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : 16;
-    c->n_gcm_nr[(nr - 10) / 2]++;
-    // kernel form: raw rounds 0..nr-1, byte-swapped last round (esp_gcm.hip)
-    for (int i = 0; i < 4 * nr; ++i) sa.rk[i] = rk[i];
+    // kernel form: raw first round, ror16 middle rounds, byte-swapped last round
+    for (int i = 0; i < 4; ++i) sa.rk[i] = rk[i];
+    for (int i = 4; i < 4 * nr; ++i) sa.rk[i] = ror16(rk[i]);
     for (int i = 0; i < 4; ++i) sa.rk[4 * nr + i] = bswap(rk[4 * nr + i]);
     uint8_t zero[16] = {0}, h[16];
     hc::aes_encrypt_block(rk, nr, zero, h);       // H = E_K(0^128), gmac.c:56-60
     std::vector<uint8_t> tabs(kGhTableBytes);
-    hc::ghash_tables(h, tabs.data());
+    hc::ghash_tables(h, kGcmLanesPerRec, tabs.data());
     HIPCHK(c, hipMemcpy(c->d_gtab + (size_t)slot * kGhTableBytes, tabs.data(), kGhTableBytes, hipMemcpyHostToDevice));
   } else {
     sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : 20;
@@ -431,7 +425,6 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
   if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
-  else c->n_gcm_nr[(c->sessions[sid].klen / 4 + 6 - 10) / 2]--;
   c->sessions[sid] = Session();
   DevSA z;
   memset(&z, 0, sizeof z);
@@ -704,7 +697,7 @@ int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_by
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
-  if (!strcmp(key, "gcm_sched")) { c->gcm_sched = value; return 0; }
+  if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ENOTSUP : 0;
   return ENOENT;
 }
 

@@ -8,10 +8,10 @@
 namespace espgpu {
 
 // ---- per-SA device record (one per session slot), 1 KiB ----------------------
-// GCM: rk[] is the AES encryption schedule in "kernel form" (esp_gcm.hip):
-//   rk[0 .. 4nr-1] raw big-endian words (rijndael-alg-fst.c layout), the last
-//   round key rk[4nr .. 4nr+3] byte-swapped (the last round emits
-//   little-endian words).  The GHASH tables live in a separate array.
+// GCM: rk[] is the AES encryption schedule in "kernel form" for the pair-table
+//   round (esp_gcm.hip): rk[0..3] raw, rk[4r..4r+3] = ror16(rk) for the
+//   middle rounds, rk[4nr..] byte-swapped (the last round emits little-endian
+//   words).  The GHASH tables live in a separate array.
 // ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
 //   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
 //   = SHA-1 chaining state after one block of key^0x36 / key^0x5c
@@ -29,17 +29,20 @@ struct DevSA {
 };
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 
-// GHASH multiplication tables for one SA (host_crypto.cpp ghash_tables), all
-// with 4-bit indices: a power's table is 32 nibble positions x 16 values x
-// 16 B = 8 KiB, nibble position j (byte j>>1 of the block in memory order,
-// low nibble if j even), value n at j*256 + n*16.
-// [0, 64 KiB)          H^1..H^8, power e at (e-1)*8 KiB (H^8 is staged into
-//                      LDS; all of them are read from L2 for the per-record
-//                      final multiply by H^(8-l));
-// [kGh16Off, +8 KiB)   H^16 (LDS, the paired Horner step).
+// GHASH multiplication tables for one SA (host_crypto.cpp ghash_tables):
+// [0, 64 KiB)          H^1..H^8 with 4-bit indices, 8 KiB per power (power e
+//                      at (e-1)*8 KiB): nibble position j (byte j>>1 of the
+//                      block in memory order, low nibble if j even), value n
+//                      at j*256 + n*16; read from L2 by the per-record final
+//                      multiply by H^(8-l);
+// [kGh8Off, +64 KiB)   H^S with 8-bit indices (S = kGcmLanesPerRec): byte
+//                      position p, value v at p*4096 + v*16 (staged into LDS,
+//                      the Horner multiplier).
+constexpr int kGcmLanesPerRec = 4;                               // GCM kernel: lanes per record
 constexpr uint32_t kGhPowerBytes = 32 * 16 * 16;                 // 8192
-constexpr uint32_t kGh16Off = 8 * kGhPowerBytes;
-constexpr uint32_t kGhTableBytes = kGh16Off + kGhPowerBytes;     // 73728
+constexpr uint32_t kGh8Off = 8 * kGhPowerBytes;
+constexpr uint32_t kGh8Bytes = 16 * 256 * 16;                    // 65536
+constexpr uint32_t kGhTableBytes = kGh8Off + kGh8Bytes;          // 131072
 
 // A chunk: up to kChunkRecs records of ONE session, processed by one
 // workgroup iteration of the GCM kernel.  rec positions index `order`
@@ -103,9 +106,8 @@ __host__ __device__ inline uint32_t esp_trailer_word(uint32_t wlast, uint32_t pl
 }
 
 // Launchers (defined in the .hip files, called by espgpu.cpp).
-// nr_mask: bit (nr-10)/2 set for each AES key size among the GCM sessions
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, uint32_t nr_mask, int sched,
-               void *stream);
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream);
+int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
 int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,

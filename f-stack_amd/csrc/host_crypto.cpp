@@ -151,16 +151,18 @@ void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
   }
 }
 
-void ghash_tables(const uint8_t h[16], uint8_t *out) {
-  // Powers H^1..H^8 (index 0..7), then H^16, each with 4-bit indices: power
-  // table p, nibble position j (byte j>>1, low nibble if j even), value n at
-  // p*8192 + j*256 + n*16 = (the block whose nibble j is n, all else 0) * H^e.
-  uint8_t pw[9][16];
+void ghash_tables(const uint8_t h[16], int stride, uint8_t *out) {
+  // Section 1 (64 KiB): powers H^1..H^8 (index 0..7) with 4-bit indices:
+  //   power p, nibble position j (byte j>>1, low nibble if j even), value n
+  //   at p*8192 + j*256 + n*16 = (the block whose nibble j is n) * H^(p+1).
+  // Section 2 (at 64 KiB): H^S with 8-bit indices (S = kGcmLanesPerRec, the
+  //   GCM kernel's Horner stride): byte position q, value v at q*4096 + v*16
+  //   = (the block whose byte q is v) * H^S.
+  uint8_t pw[8][16];
   memcpy(pw[0], h, 16);
   for (int p = 1; p < 8; ++p) gf128_mul(pw[p - 1], h, pw[p]);
-  gf128_mul(pw[7], pw[7], pw[8]);                      // H^16
-  for (int p = 0; p < 9; ++p) {
-    // products of every single-bit block with the power
+  for (int p = 0; p < 8; ++p) {
+    // products of every single-bit block with H^(p+1)
     uint8_t bit[128][16];
     for (int b = 0; b < 128; ++b) {
       uint8_t e[16] = {0};
@@ -178,6 +180,15 @@ void ghash_tables(const uint8_t h[16], uint8_t *out) {
       }
     }
   }
+  // the 8-bit H^S table from the 4-bit H^S one (GF(2)-linear in the block)
+  const uint8_t *h8 = out + (size_t)(stride - 1) * 8192;
+  uint8_t *t8 = out + 8 * 8192;
+  for (int q = 0; q < 16; ++q)
+    for (int v = 0; v < 256; ++v) {
+      const uint8_t *lo = h8 + (2 * q) * 256 + (v & 15) * 16;
+      const uint8_t *hi = h8 + (2 * q + 1) * 256 + (v >> 4) * 16;
+      for (int k = 0; k < 16; ++k) t8[(size_t)q * 4096 + (size_t)v * 16 + k] = lo[k] ^ hi[k];
+    }
 }
 
 void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {

@@ -25,8 +25,9 @@ void aes_encrypt_block(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t
 void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
 
 // GHASH table set for the GCM kernel (kGhTableBytes, espgpu_internal.h):
-// H^1..H^8 then H^16, 8 KiB each, with 4-bit indices.
-void ghash_tables(const uint8_t h[16], uint8_t *out);
+// H^1..H^8 with 4-bit indices (8 KiB each), then H^stride with 8-bit
+// indices (64 KiB); stride = the kernel's lanes per record (1..8).
+void ghash_tables(const uint8_t h[16], int stride, uint8_t *out);
 
 // SHA-1 compression of one 64-byte block into state h[5].
 void sha1_compress(uint32_t h[5], const uint8_t block[64]);

@@ -7,15 +7,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_ghash_table_layout_selftest(tmp_path):
-    """The 4-bit H^1..H^8 and H^16 GHASH tables the GCM kernel indexes, and its
-    paired stride-8 Horner + final H^(8-l) combination, against gf128_mul and
-    a serial GHASH (tools/ghash_selftest.cpp)."""
+    """The 8-bit H^8 (LDS) and 4-bit H^1..H^8 (global) GHASH tables the GCM
+    kernel indexes, and its stride-8 Horner + final H^(8-l) combination,
+    against gf128_mul and a serial GHASH (tools/ghash_selftest.cpp)."""
     import re
     hdr = open(os.path.join(ROOT, "f-stack_amd", "csrc", "espgpu_internal.h")).read()
     # the self-test mirrors these constants; keep them in step with the header
     assert re.search(r"kGhPowerBytes = 32 \* 16 \* 16;", hdr)
-    assert re.search(r"kGh16Off = 8 \* kGhPowerBytes;", hdr)
-    assert re.search(r"kGhTableBytes = kGh16Off \+ kGhPowerBytes;", hdr)
+    assert re.search(r"kGh8Off = 8 \* kGhPowerBytes;", hdr)
+    assert re.search(r"kGh8Bytes = 16 \* 256 \* 16;", hdr)
+    assert re.search(r"kGhTableBytes = kGh8Off \+ kGh8Bytes;", hdr)
     exe = tmp_path / "ghash_selftest"
     csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Kernel-time A/B harness for the GCM decrypt kernel (measurement only).
 
-  python tools/gcm_timing.py [--records N] [--rec-len L] [--reps R] [--sched S ...]
+  python tools/gcm_timing.py [--records N] [--rec-len L] [--reps R] [--opts K ...]
 
 Times espgpu_decrypt_batch (out of place, grouped, one AES-128-GCM SA) over N
 random records of L bytes with HIP events on the launch stream, once per
-schedule variant.  Records are random bytes, not valid ESP: every tag check
+measurement-knob setting.  Records are random bytes, not valid ESP: every tag check
 fails, which is the same work as a passing one (the kernel decrypts
 regardless in out-of-place mode), so a variant whose arithmetic is
 deliberately wrong can still be timed.  Prints one JSON line per variant."""
@@ -25,7 +25,9 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 20)
     ap.add_argument("--rec-len", type=int, default=1480)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--sched", type=int, nargs="*", default=[0])
+    ap.add_argument("--opts", type=int, nargs="*", default=[0],
+                    help="measurement knobs (libespgpu built with make KNOBS=1): 1 no loads/stores, "
+                         "2 no GHASH, 4 no AES rounds 3+")
     ap.add_argument("--grid", type=int, default=0)
     args = ap.parse_args()
     import torch
@@ -48,8 +50,9 @@ def main():
     stream = torch.cuda.Stream()
     algo = n * (rl + 16) + n * (rl - 32) + n
     drv.lib.espgpu_set_tuning(drv.ctx, b"grid", args.grid)
-    for s in args.sched:
-        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_sched", s)
+    for s in args.opts:
+        if s:
+            assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_opts", s) == 0, "knobs need a KNOBS=1 build"
         with torch.cuda.stream(stream):
             for _ in range(3):
                 decrypt_batch(drv, arena, desc, n, st, out=out, grouped=True, stream=stream)
@@ -60,7 +63,7 @@ def main():
             e1.record(stream)
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(json.dumps({"sched": s, "grid": args.grid, "records": n, "rec_len": rl, "kernel_ms": round(ms, 4),
+        print(json.dumps({"opts": s, "grid": args.grid, "records": n, "rec_len": rl, "kernel_ms": round(ms, 4),
                           "algo_GBps": round(algo / ms / 1e6, 1)}), flush=True)
     drv.close()
 
