@@ -10,31 +10,35 @@
 //           len - 16 - mlen bytes (cryptosoft.c:1112-1117 honours mlen < 16).
 //
 // Mapping (MI355X-first, not a translation of the 16-byte-at-a-time loop):
-//  * 8 lanes per ESP record, 8 records per wave, 16 waves per workgroup
-//    (a 128-record "chunk" of ONE session per workgroup iteration).
+//  * S = kGcmLanesPerRec = 4 lanes per ESP record, 16 records per wave, 16
+//    waves per workgroup, one workgroup per CU (128 KiB LDS); workgroups take
+//    256-record chunks of ONE session from a ticket counter.
 //  * GHASH is reassociated so every lane runs a Horner chain with the SAME
-//    multiplier H^8 over blocks l, l+8, l+16, ... of its record (the block list
-//    is front-padded with zero blocks to a multiple of 8, which leaves the hash
-//    unchanged), then multiplies by H^(8-l) and the 8 partials are XOR-reduced
-//    across the lane group.  Multiplication by a fixed H^e uses tables indexed
-//    per byte or nibble POSITION, so there is no shift/reduce step:
-//    X*H^e = XOR_j T_e[j][digit_j(X)].  The Horner multiplier H^8 is in LDS
-//    with 8-bit indices (16 lookups per block); the per-lane final H^(8-l) is
-//    gathered from L2 (4-bit tables).  Measured against a conflict-free 4-bit
-//    H^8/H^16 pair in LDS with four T-tables: this layout reads
-//    half the GHASH rows, which outweighs its bank conflicts.
+//    multiplier H^S over blocks l, l+S, l+2S, ... of its record (the block
+//    list is front-padded with zero blocks to a multiple of S, which leaves
+//    the hash unchanged), then multiplies by H^(S-l) and the S partials are
+//    XOR-reduced across the lane group.  Multiplication by a fixed H^e uses
+//    tables indexed per byte or nibble POSITION, so there is no shift/reduce
+//    step: X*H^e = XOR_j T_e[j][digit_j(X)].  The Horner multiplier H^S is in
+//    LDS with 8-bit indices (16 ds_read_b128 per block); the per-lane final
+//    H^(S-l) is gathered from L2 (4-bit tables).  Measured against a
+//    conflict-free 4-bit layout with four T-tables: this layout
+//    reads half the GHASH rows, which outweighs its bank conflicts.
 //  * AES-CTR uses T-tables Te0 and Te1 replicated 32x in LDS (entry x at x*256:
 //    Te0 in lane slots (lane&31)*4, Te1 128 bytes later): ds_read_b32 with every
 //    lane of a 32-lane group on its own bank -> conflict-free; the LDS address
 //    is a single v_perm_b32 of (state byte, lane slot).  Te2/Te3 are folded
 //    through one ror16 per column: t = Te0[a]^Te1[b]^ror16(Te0[c]^Te1[d]^ror16(rk)).
+//    Rounds 1-2 come from a per-lane cache keyed on ctr>>8 (counter mode only
+//    changes the low byte inside 256 blocks).
 //  * The lane that owns GHASH block i also computes AES(nonce||i+1): block 0
 //    (the AAD block) gets J0, CT block c = i-1 gets counter c+2, so the CTR
-//    work is perfectly aligned with the hash work and plaintext is stored from
-//    the same registers that fed GHASH.
-//  * Records and descriptors are read with 16-byte loads, 128 contiguous bytes
-//    per lane group per step.  HBM traffic per record = record + descriptor +
-//    plaintext + status byte.
+//    work is aligned with the hash work and plaintext is stored from the same
+//    registers that fed GHASH.  Steps run in pairs (blocks i and i+S: two
+//    independent AES states per lane, GHASH (Y*H^S ^ Ba)*H^S ^ Bb).
+//  * Records are read and written with single 16-byte vector accesses, 128
+//    contiguous bytes per record per paired step.  HBM traffic per record =
+//    record + descriptor + plaintext + status byte.
 #include <hip/hip_runtime.h>
 
 #include "espgpu_internal.h"
@@ -69,13 +73,21 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 __device__ __forceinline__ uint32_t ror16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return perm(x, x, 0x00010203u); }
 
+// 16- and 8-byte accesses at 4-byte alignment as single vector memory
+// operations (one IR access each, so the backend never splits or re-merges them)
+typedef uint32_t V4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t V2a __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-  U4 v = *reinterpret_cast<const U4 *>(p);
+  const V4a v = *reinterpret_cast<const V4a *>(p);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
-  U4 u{v.x, v.y, v.z, v.w};
-  *reinterpret_cast<U4 *>(p) = u;
+  V4a u = {v.x, v.y, v.z, v.w};
+  *reinterpret_cast<V4a *>(p) = u;
+}
+__device__ __forceinline__ void st8(uint8_t *p, uint32_t a, uint32_t b) {
+  V2a u = {a, b};
+  *reinterpret_cast<V2a *>(p) = u;
 }
 
 // Keep the first `rem` bytes of a 16-byte block, zero the rest.  Valid ESP
@@ -91,10 +103,14 @@ __device__ __forceinline__ void st_partial(uint8_t *p, uint4 v, int rem) {
     st16(p, v);
     return;
   }
-  uint32_t *q = reinterpret_cast<uint32_t *>(p);
-  q[0] = v.x;
-  if (rem > 4) q[1] = v.y;
-  if (rem > 8) q[2] = v.z;
+  // the last block of a record: 4, 8 or 12 bytes, no store shared with the
+  // full-block path (a common first-word store would be hoisted out of both
+  // branches and split every full block into three stores)
+  if (rem > 4)
+    st8(p, v.x, v.y);
+  else
+    *reinterpret_cast<uint32_t *>(p) = v.x;
+  if (rem > 8) *reinterpret_cast<uint32_t *>(p + 8) = v.z;
 }
 
 // ---- AES (rijndaelEncrypt, rijndael-alg-fst.c:863-1042) on the pair table ----
@@ -137,7 +153,8 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
 
 // Measurement knobs, compiled in only by `make KNOBS=1` (tools/gcm_timing.py
 // --opts): bit0 skips the record loads and plaintext stores, bit1 the GHASH
-// multiplies, bit2 the AES rounds after round 2.  They break results on
+// multiplies, bit2 the AES rounds after round 2, bit3 the stores only, bit4
+// the loads only.  They break results on
 // purpose, to split the kernel's time between memory, GHASH and AES.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t g_opts;
@@ -398,7 +415,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       }
       if (MODE == 0) {
         const uint4 pt = xor4(C, ks);
-        if (!(gopts() & 1)) st_partial(orec + 16 + 16 * c, pt, rem);
+        if (!(gopts() & 9)) st_partial(orec + 16 + 16 * c, pt, rem);
         note_trailer(i, pt, rem);
       }
       return mask_block(C, rem);
@@ -422,8 +439,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         const int ib = i + S;
         const bool hca = valid && i >= 1 && i <= nct, hcb = valid && ib <= nct;
         uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
-        if (hca && !(gopts() & 1)) Ca = ld16(rec + 16 * i);
-        if (hcb && !(gopts() & 1)) Cb = ld16(rec + 16 * ib);
+        if (hca && !(gopts() & 17)) Ca = ld16(rec + 16 * i);
+        if (hcb && !(gopts() & 17)) Cb = ld16(rec + 16 * ib);
         uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
         if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
         uint4 Ba;
