@@ -9,7 +9,6 @@
 //   freesession   cryptosoft.c:1412
 //   process       cryptosoft.c:1429-1441 (swcr_process) -> swcr_gcm :465 / swcr_eta :874
 //   completion    crypto_done, crypto.c:1802
-#include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -23,10 +22,6 @@
 #include "espgpu.h"
 #include "espgpu_internal.h"
 #include "host_crypto.h"
-
-#ifndef ERESTART
-#define ERESTART 85   /* FreeBSD's value is -1 in-kernel; Linux has 85. */
-#endif
 
 using namespace espgpu;
 
@@ -47,7 +42,7 @@ struct Pending {
   // receives staged bytes [stage_from, stage_from+n); up to 2 spans
   struct Span { uint32_t buf_off, stage_from, n; } span[2];
   int nspan;
-  std::vector<espgpu_seg> segs;
+  uint32_t seg0, nsegs;       // the request's segments, copied into Slot::segpool
 };
 
 enum { SLOT_FREE = 0, SLOT_FILLING = 1, SLOT_INFLIGHT = 2 };
@@ -59,7 +54,8 @@ struct Slot {
   espgpu_desc *h_desc = nullptr, *d_desc = nullptr;
   uint8_t *h_status = nullptr, *d_status = nullptr;
   uint32_t nrec = 0, bytes = 0;
-  std::vector<Pending> reqs;
+  std::vector<Pending> reqs;             // reserved to batch_records: no per-record allocation
+  std::vector<espgpu_seg> segpool;       // segment lists of the staged requests
   hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
 };
 
@@ -94,7 +90,16 @@ struct espgpu_ctx {
   // staging
   std::vector<Slot> slots;
   int cur = 0;
-  std::vector<espgpu_completion> ready;   // host-side completions (EINVAL etc.)
+  // completions not yet handed to poll(): ready[ready_head..] (host-side
+  // rejects and finished batches), reserved so steady state does not allocate
+  std::vector<espgpu_completion> ready;
+  size_t ready_head = 0;
+  // the stream the ctx last launched on and an event after that launch: the
+  // work-queue counters and planner workspace are per ctx, so a launch on a
+  // different stream first waits for it (stream-ordered, never concurrent)
+  hipStream_t last_st = nullptr;
+  bool launched = false;
+  hipEvent_t ev_last = nullptr;
   espgpu_stats stats{};
   float last_ms = 0.f;
   std::string err;
@@ -117,7 +122,7 @@ int fail(espgpu_ctx *c, int code, const char *fmt, ...) {
 #define HIPCHK(ctx, expr)                                                          \
   do {                                                                             \
     hipError_t e_ = (expr);                                                        \
-    if (e_ != hipSuccess) return fail(ctx, EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
+    if (e_ != hipSuccess) return fail(ctx, ESPGPU_EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
 uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
@@ -144,8 +149,9 @@ int ensure_plan(espgpu_ctx *c, uint32_t n) {
 }
 
 // Copy `n` bytes at logical offset `off` of a segmented buffer.
-bool seg_copy_out(const std::vector<espgpu_seg> &segs, uint32_t off, uint32_t n, uint8_t *dst) {
-  for (const auto &s : segs) {
+bool seg_copy_out(const espgpu_seg *segs, uint32_t nsegs, uint32_t off, uint32_t n, uint8_t *dst) {
+  for (uint32_t i = 0; i < nsegs; ++i) {
+    const espgpu_seg &s = segs[i];
     if (off >= s.len) { off -= s.len; continue; }
     uint32_t k = std::min(n, s.len - off);
     memcpy(dst, (const uint8_t *)s.base + off, k);
@@ -154,8 +160,9 @@ bool seg_copy_out(const std::vector<espgpu_seg> &segs, uint32_t off, uint32_t n,
   }
   return n == 0;
 }
-bool seg_copy_in(const std::vector<espgpu_seg> &segs, uint32_t off, uint32_t n, const uint8_t *src) {
-  for (const auto &s : segs) {
+bool seg_copy_in(const espgpu_seg *segs, uint32_t nsegs, uint32_t off, uint32_t n, const uint8_t *src) {
+  for (uint32_t i = 0; i < nsegs; ++i) {
+    const espgpu_seg &s = segs[i];
     if (off >= s.len) { off -= s.len; continue; }
     uint32_t k = std::min(n, s.len - off);
     memcpy((uint8_t *)s.base + off, src, k);
@@ -178,6 +185,8 @@ int alloc_slot(espgpu_ctx *c, Slot &s) {
   HIPCHK(c, hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming));
   HIPCHK(c, hipEventCreate(&s.k0));
   HIPCHK(c, hipEventCreate(&s.k1));
+  s.reqs.reserve(recs);
+  s.segpool.reserve(recs * 2);
   return 0;
 }
 
@@ -193,6 +202,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
               uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st,
               uint32_t *d_trailer = nullptr) {
   if (n == 0) return 0;
+  if (c->launched && st != c->last_st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
   const uint32_t nsas = (uint32_t)c->sessions.size();
   GcmParams p{};
   p.arena = d_arena;
@@ -211,13 +221,13 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     if (e) return e;
     if (launch_plan(d_desc, n, c->d_sas, nsas, c->d_work, c->d_order, c->d_chunks, c->d_nchunks,
                     c->max_chunks, st))
-      return fail(c, ENOTSUP, "planner: too many sessions for device grouping (%u); pre-group and pass ESPGPU_BATCH_GROUPED", nsas);
+      return fail(c, ESPGPU_ENOTSUP, "planner: too many sessions for device grouping (%u); pre-group and pass ESPGPU_BATCH_GROUPED", nsas);
     p.order = c->d_order;
     p.chunks = c->d_chunks;
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st)) return fail(c, EIO, "GCM kernel launch failed");
+  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if (c->n_eta > 0) {
     EtaParams q{};
     q.arena = d_arena;
@@ -235,8 +245,11 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.isbox = c->d_isbox;
     q.status = d_status;
     q.nsas = nsas;
-    if (launch_eta(q, encrypt, (int)c->cfg.grid, st)) return fail(c, EIO, "ETA kernel launch failed");
+    if (launch_eta(q, encrypt, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
+  HIPCHK(c, hipEventRecord(c->ev_last, st));
+  c->last_st = st;
+  c->launched = true;
   return 0;
 }
 
@@ -249,7 +262,7 @@ int espgpu_abi_version(void) { return ESPGPU_ABI_VERSION; }
 const char *espgpu_last_error(espgpu_ctx *c) { return c ? c->err.c_str() : "no context"; }
 
 int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
-  if (!out) return EINVAL;
+  if (!out) return ESPGPU_EINVAL;
   *out = nullptr;
   espgpu_ctx *c = new espgpu_ctx();
   espgpu_config cfg{};
@@ -264,14 +277,14 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
   do {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg.device) {
-      rc = fail(c, ENODEV, "no HIP device %d (found %d)", cfg.device, ndev);
+      rc = fail(c, ESPGPU_ENODEV, "no HIP device %d (found %d)", cfg.device, ndev);
       break;
     }
-    if (hipSetDevice(cfg.device) != hipSuccess) { rc = fail(c, ENODEV, "hipSetDevice failed"); break; }
+    if (hipSetDevice(cfg.device) != hipSuccess) { rc = fail(c, ESPGPU_ENODEV, "hipSetDevice failed"); break; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
-      rc = fail(c, EIO, "stream");
+      rc = fail(c, ESPGPU_EIO, "stream");
       break;
     }
     for (int k = 0; k < 2; ++k) {
@@ -280,13 +293,15 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     }
     hipEventCreate(&c->ev0);
     hipEventCreate(&c->ev1);
+    hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming);
+    c->ready.reserve((size_t)cfg.batch_records * cfg.nbatches + 1024);
     if (hipMalloc(&c->d_sas, (size_t)cfg.max_sessions * sizeof(DevSA)) != hipSuccess ||
         hipMalloc(&c->d_gtab, (size_t)cfg.max_sessions * kGhTableBytes) != hipSuccess ||
         hipMalloc(&c->d_tpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_dpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_isbox, 256) != hipSuccess ||
         hipMalloc(&c->d_queue, 16) != hipSuccess) {
-      rc = fail(c, ENOMEM, "device SA table allocation failed");
+      rc = fail(c, ESPGPU_ENOMEM, "device SA table allocation failed");
       break;
     }
     hipMemset(c->d_sas, 0, (size_t)cfg.max_sessions * sizeof(DevSA));
@@ -328,6 +343,7 @@ void espgpu_fini(espgpu_ctx *c) {
   hipFree(c->d_work); hipFree(c->d_order); hipFree(c->d_chunks); hipFree(c->d_nchunks);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->ev_last) hipEventDestroy(c->ev_last);
   for (hipStream_t st : {c->s_in, c->stream, c->s_out})
     if (st) hipStreamDestroy(st);
   delete c;
@@ -335,45 +351,45 @@ void espgpu_fini(espgpu_ctx *c) {
 
 // swcr_probesession + check_csp restricted to the ESP ciphers this engine serves.
 int espgpu_probesession(const espgpu_session_params *csp) {
-  if (!csp) return EINVAL;
+  if (!csp) return ESPGPU_EINVAL;
   const int supported_flags = ESPGPU_CSP_F_SEPARATE_AAD | ESPGPU_CSP_F_ESN;
-  if (csp->csp_flags & ~supported_flags) return EINVAL;
+  if (csp->csp_flags & ~supported_flags) return ESPGPU_EINVAL;
   if (csp->csp_ivlen < 0 || csp->csp_cipher_klen < 0 || csp->csp_auth_klen < 0 || csp->csp_auth_mlen < 0)
-    return EINVAL;
+    return ESPGPU_EINVAL;
   const int k = csp->csp_cipher_klen;
   const bool aes_klen = (k == 16 || k == 24 || k == 32);
   switch (csp->csp_mode) {
     case ESPGPU_CSP_MODE_AEAD:
-      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_NIST_GCM_16 || !aes_klen) return EINVAL;
-      if (csp->csp_ivlen != 12) return EINVAL;                 // cryptosoft.c:1093
-      if (csp->csp_auth_alg != 0 || csp->csp_auth_klen != 0) return EINVAL;
+      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_NIST_GCM_16 || !aes_klen) return ESPGPU_EINVAL;
+      if (csp->csp_ivlen != 12) return ESPGPU_EINVAL;                 // cryptosoft.c:1093
+      if (csp->csp_auth_alg != 0 || csp->csp_auth_klen != 0) return ESPGPU_EINVAL;
       // ICVs of 8/12/16 bytes (RFC 4106 s3.3); the kernels move whole dwords,
-      // so other truncations are left to cryptosoft (probe EINVAL)
-      if (csp->csp_auth_mlen > 16 || (csp->csp_auth_mlen & 3)) return EINVAL;
-      if (csp->csp_flags & ESPGPU_CSP_F_ESN) return EINVAL;    // ESN for GCM = SEPARATE_AAD
+      // so other truncations are left to cryptosoft (probe ESPGPU_EINVAL)
+      if (csp->csp_auth_mlen > 16 || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
+      if (csp->csp_flags & ESPGPU_CSP_F_ESN) return ESPGPU_EINVAL;    // ESN for GCM = SEPARATE_AAD
       return ESPGPU_PROBE_HARDWARE;
     case ESPGPU_CSP_MODE_ETA:
-      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC || !aes_klen) return EINVAL;
-      if (csp->csp_ivlen != 16) return EINVAL;
-      if (csp->csp_auth_alg != ESPGPU_CRYPTO_SHA1_HMAC || csp->csp_auth_klen <= 0) return EINVAL;
-      if (csp->csp_auth_mlen > 20 || (csp->csp_auth_mlen & 3)) return EINVAL;
-      if (csp->csp_flags & ESPGPU_CSP_F_SEPARATE_AAD) return EINVAL;
+      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC || !aes_klen) return ESPGPU_EINVAL;
+      if (csp->csp_ivlen != 16) return ESPGPU_EINVAL;
+      if (csp->csp_auth_alg != ESPGPU_CRYPTO_SHA1_HMAC || csp->csp_auth_klen <= 0) return ESPGPU_EINVAL;
+      if (csp->csp_auth_mlen > 20 || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
+      if (csp->csp_flags & ESPGPU_CSP_F_SEPARATE_AAD) return ESPGPU_EINVAL;
       return ESPGPU_PROBE_HARDWARE;
     default:
-      return EINVAL;
+      return ESPGPU_EINVAL;
   }
 }
 
 int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *sid_out) {
-  if (!c || !csp || !sid_out) return EINVAL;
+  if (!c || !csp || !sid_out) return ESPGPU_EINVAL;
   int pr = espgpu_probesession(csp);
-  if (pr >= 0) return fail(c, EINVAL, "session parameters not supported");
-  if (!csp->csp_cipher_key) return fail(c, EINVAL, "per-request keys are not supported; session key required");
+  if (pr >= 0) return fail(c, ESPGPU_EINVAL, "session parameters not supported");
+  if (!csp->csp_cipher_key) return fail(c, ESPGPU_EINVAL, "per-request keys are not supported; session key required");
   int slot = -1;
   for (size_t i = 0; i < c->sessions.size(); ++i)
     if (!c->sessions[i].used) { slot = (int)i; break; }
   if (slot < 0) {
-    if (c->sessions.size() >= c->cfg.max_sessions) return fail(c, ENOMEM, "SA table full (%u)", c->cfg.max_sessions);
+    if (c->sessions.size() >= c->cfg.max_sessions) return fail(c, ESPGPU_ENOMEM, "SA table full (%u)", c->cfg.max_sessions);
     slot = (int)c->sessions.size();
     c->sessions.emplace_back();
     c->h_sas.emplace_back();
@@ -421,7 +437,9 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
 
 void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   if (!c || sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return;
-  // Records already flushed keep their results; wait so the slot is not reused under them.
+  // Requests already staged were accepted under this key: launch them now,
+  // then wait, so neither they nor flushed batches see the slot reused.
+  espgpu_flush(c);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
   if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
@@ -435,64 +453,65 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
 // (xform_esp.c:364-461, 820-900) and stage it as an ESP wire record.
 int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   (void)hint;
-  if (!c || !r) return EINVAL;
+  if (!c || !r) return ESPGPU_EINVAL;
   Slot *s = &c->slots[c->cur];
-  if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ERESTART; }
+  if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ESPGPU_ERESTART; }
   const int op = (r->crp_op & ESPGPU_CRYPTO_OP_ENCRYPT) ? 1 : 0;
   if (s->state == SLOT_FILLING && s->op != op) {
     int e = espgpu_flush(c);
     if (e) return e;
     s = &c->slots[c->cur];
-    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ERESTART; }
+    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ESPGPU_ERESTART; }
   }
   auto reject = [&](int etype) {
     c->ready.push_back(espgpu_completion{r->opaque, etype});
-    if (etype == EINVAL) c->stats.einval++;
+    if (etype == ESPGPU_EINVAL) c->stats.einval++;
     return 0;
   };
   const int sid = r->session;
-  if (sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return reject(EINVAL);
+  if (sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return reject(ESPGPU_EINVAL);
   const Session &ses = c->sessions[sid];
   size_t total = 0;
   for (int i = 0; i < r->nsegs; ++i) total += r->segs[i].len;
   const bool gcm = ses.mode == ESPGPU_CSP_MODE_AEAD;
-  const int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen, alen = gcm ? 16 : ses.mlen;
+  // ICV bytes in the record: the session's (possibly truncated) mlen, 16/12/8
+  // for GCM (cryptosoft.c:1112-1117), 12 or 20 for HMAC-SHA1
+  const int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen, alen = ses.mlen;
   const int plen = r->crp_payload_length;
   int aad_start = r->crp_aad_start;
   // ESP shape checks
-  if (plen <= 0 || r->crp_payload_start < 0 || (size_t)(r->crp_digest_start + alen) > total) return reject(EINVAL);
+  if (plen <= 0 || r->crp_payload_start < 0 || (size_t)(r->crp_digest_start + alen) > total) return reject(ESPGPU_EINVAL);
   uint8_t hdr[8];
   uint32_t esn_hi = 0, salt = 0;
   if (gcm) {
-    if (!(r->crp_flags & ESPGPU_CRYPTO_F_IV_SEPARATE)) return reject(EINVAL);   // cryptosoft.c:496
+    if (!(r->crp_flags & ESPGPU_CRYPTO_F_IV_SEPARATE)) return reject(ESPGPU_EINVAL);   // cryptosoft.c:496
     if (r->crp_aad) {
-      if (!(ses.flags & ESPGPU_CSP_F_SEPARATE_AAD) || r->crp_aad_length != 12) return reject(EINVAL);
+      if (!(ses.flags & ESPGPU_CSP_F_SEPARATE_AAD) || r->crp_aad_length != 12) return reject(ESPGPU_EINVAL);
       const uint8_t *a = (const uint8_t *)r->crp_aad;
       memcpy(hdr, a, 4);
       memcpy(hdr + 4, a + 8, 4);
       esn_hi = be32(a + 4);
       aad_start = r->crp_payload_start - hlen;   // header bytes in the buffer (unused by the cipher)
     } else {
-      if (r->crp_aad_length != 8 || (ses.flags & ESPGPU_CSP_F_SEPARATE_AAD)) return reject(EINVAL);
-      if (r->crp_payload_start != aad_start + hlen) return reject(EINVAL);
-      std::vector<espgpu_seg> sv(r->segs, r->segs + r->nsegs);
-      if (!seg_copy_out(sv, (uint32_t)aad_start, 8, hdr)) return reject(EINVAL);
+      if (r->crp_aad_length != 8 || (ses.flags & ESPGPU_CSP_F_SEPARATE_AAD)) return reject(ESPGPU_EINVAL);
+      if (r->crp_payload_start != aad_start + hlen) return reject(ESPGPU_EINVAL);
+      if (!seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)aad_start, 8, hdr)) return reject(ESPGPU_EINVAL);
     }
     salt = le32(r->crp_iv);
   } else {
     if (r->crp_aad || r->crp_aad_length != hlen || r->crp_iv_start != aad_start + 8 ||
         r->crp_payload_start != aad_start + hlen || (plen & 15))
-      return reject(EINVAL);
+      return reject(ESPGPU_EINVAL);
     if (ses.flags & ESPGPU_CSP_F_ESN) esn_hi = be32(r->crp_esn);
   }
-  if (r->crp_digest_start != r->crp_payload_start + plen) return reject(EINVAL);
+  if (r->crp_digest_start != r->crp_payload_start + plen) return reject(ESPGPU_EINVAL);
   const uint32_t rlen = (uint32_t)(hlen + plen + alen);
-  if (rlen > 65535 || (rlen & 3)) return reject(EINVAL);
+  if (rlen > 65535 || (rlen & 3)) return reject(ESPGPU_EINVAL);
   if (s->nrec >= c->cfg.batch_records || s->bytes + rlen + 16 > c->cfg.batch_bytes) {
     int e = espgpu_flush(c);
     if (e) return e;
     s = &c->slots[c->cur];
-    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ERESTART; }
+    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ESPGPU_ERESTART; }
   }
   if (s->state == SLOT_FREE) {
     s->state = SLOT_FILLING;
@@ -500,6 +519,7 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
     s->nrec = 0;
     s->bytes = 0;
     s->reqs.clear();
+    s->segpool.clear();
   }
   Pending pd;
   pd.opaque = r->opaque;
@@ -507,17 +527,19 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   pd.rec = s->nrec;
   pd.stage_off = s->bytes;
   pd.stage_len = rlen;
-  pd.segs.assign(r->segs, r->segs + r->nsegs);
   uint8_t *dst = s->h_arena + s->bytes;
   bool ok;
   if (gcm) {
     memcpy(dst, hdr, 8);
     memcpy(dst + 8, r->crp_iv + 4, 8);
-    ok = seg_copy_out(pd.segs, (uint32_t)r->crp_payload_start, (uint32_t)(plen + alen), dst + hlen);
+    ok = seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)r->crp_payload_start, (uint32_t)(plen + alen), dst + hlen);
   } else {
-    ok = seg_copy_out(pd.segs, (uint32_t)aad_start, rlen, dst);
+    ok = seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)aad_start, rlen, dst);
   }
-  if (!ok) return reject(EINVAL);
+  if (!ok) return reject(ESPGPU_EINVAL);
+  pd.seg0 = (uint32_t)s->segpool.size();
+  pd.nsegs = (uint32_t)r->nsegs;
+  s->segpool.insert(s->segpool.end(), r->segs, r->segs + r->nsegs);
   // results: payload (+ digest when encrypting) go back to the request buffer
   pd.nspan = 1;
   pd.span[0] = {(uint32_t)r->crp_payload_start, (uint32_t)hlen, (uint32_t)plen};
@@ -533,12 +555,12 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   d.salt = salt;
   s->bytes += (rlen + 15) & ~15u;
   s->nrec++;
-  s->reqs.push_back(std::move(pd));
+  s->reqs.push_back(pd);
   return 0;
 }
 
 int espgpu_flush(espgpu_ctx *c) {
-  if (!c) return EINVAL;
+  if (!c) return ESPGPU_EINVAL;
   Slot &s = c->slots[c->cur];
   if (s.state != SLOT_FILLING || s.nrec == 0) return 0;
   // H2D on s_in -> kernels on the compute stream -> D2H on s_out, chained by
@@ -572,9 +594,10 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
     if (et == 0) {
       const uint8_t *src = s.h_arena + pd.stage_off;
       for (int k = 0; k < pd.nspan; ++k)
-        seg_copy_in(pd.segs, pd.span[k].buf_off, pd.span[k].n, src + pd.span[k].stage_from);
+        seg_copy_in(s.segpool.data() + pd.seg0, pd.nsegs, pd.span[k].buf_off, pd.span[k].n,
+                    src + pd.span[k].stage_from);
       c->stats.bytes += pd.span[0].n;
-    } else if (et == EBADMSG) {
+    } else if (et == ESPGPU_EBADMSG) {
       c->stats.auth_fail++;
     } else {
       c->stats.einval++;
@@ -583,6 +606,7 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
     c->ready.push_back(espgpu_completion{pd.opaque, et});
   }
   s.reqs.clear();
+  s.segpool.clear();
   s.nrec = 0;
   s.bytes = 0;
   s.state = SLOT_FREE;
@@ -590,7 +614,7 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
 }
 
 int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
-  if (!c) return -EINVAL;
+  if (!c) return -ESPGPU_EINVAL;
   // completions of flushed batches, oldest first
   for (size_t k = 0; k < c->slots.size(); ++k) {
     Slot &s = c->slots[(c->cur + k) % c->slots.size()];
@@ -598,14 +622,19 @@ int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
     if (hipEventQuery(s.done) != hipSuccess) continue;
     complete_slot(c, s);
   }
-  int n = std::min<int>(max, (int)c->ready.size());
-  for (int i = 0; i < n; ++i) out[i] = c->ready[i];
-  c->ready.erase(c->ready.begin(), c->ready.begin() + n);
+  const int avail = (int)(c->ready.size() - c->ready_head);
+  const int n = std::min(max, avail);
+  for (int i = 0; i < n; ++i) out[i] = c->ready[c->ready_head + i];
+  c->ready_head += n;
+  if (c->ready_head == c->ready.size()) {
+    c->ready.clear();
+    c->ready_head = 0;
+  }
   return n;
 }
 
 int espgpu_drain(espgpu_ctx *c) {
-  if (!c) return EINVAL;
+  if (!c) return ESPGPU_EINVAL;
   int e = espgpu_flush(c);
   if (e) return e;
   HIPCHK(c, hipStreamSynchronize(c->s_out));
@@ -615,14 +644,14 @@ int espgpu_drain(espgpu_ctx *c) {
 }
 
 int espgpu_get_stats(espgpu_ctx *c, espgpu_stats *st) {
-  if (!c || !st) return EINVAL;
+  if (!c || !st) return ESPGPU_EINVAL;
   *st = c->stats;
   return 0;
 }
 
 int espgpu_decrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
                          uint8_t *d_status, uint8_t *d_out, uint32_t flags, void *stream) {
-  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return EINVAL;
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return ESPGPU_EINVAL;
   return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
                    reinterpret_cast<hipStream_t>(stream));
 }
@@ -630,14 +659,14 @@ int espgpu_decrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_d
 int espgpu_decrypt_batch_trailer(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc,
                                  uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t *d_trailer,
                                  uint32_t flags, void *stream) {
-  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_trailer && n)) return EINVAL;
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_trailer && n)) return ESPGPU_EINVAL;
   return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
                    reinterpret_cast<hipStream_t>(stream), d_trailer);
 }
 
 int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
                          uint8_t *d_status, uint32_t flags, void *stream) {
-  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return EINVAL;
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return ESPGPU_EINVAL;
   return run_batch(c, d_arena, d_desc, n, d_status, nullptr, flags, 1, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -646,7 +675,7 @@ float espgpu_last_kernel_ms(espgpu_ctx *c) { return c ? c->last_ms : 0.f; }
 static int host_pipeline(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_bytes,
                          const espgpu_desc *h_desc, uint32_t n, uint8_t *h_status, uint8_t *h_out,
                          uint32_t chunk, uint32_t flags, int encrypt) {
-  if (!c || !h_arena || !h_desc || !h_status || (!encrypt && !h_out)) return EINVAL;
+  if (!c || !h_arena || !h_desc || !h_status || (!encrypt && !h_out)) return ESPGPU_EINVAL;
   if (n == 0) return 0;
   if (!chunk) chunk = 65536;
   if (arena_bytes + 64 > c->e2e_bytes || n > c->e2e_n) {
@@ -695,10 +724,10 @@ int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_by
 }
 
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
-  if (!c || !key) return EINVAL;
+  if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
-  if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ENOTSUP : 0;
-  return ENOENT;
+  if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
+  return ESPGPU_ENOENT;
 }
 
 }  // extern "C"

@@ -19,12 +19,15 @@ IPPROTO_NONE = 59
 class SecAssoc:
     """What key_setsaval leaves in struct secasvar for the two ESP transforms."""
 
-    def __init__(self, spi, alg, key, auth_key=b"", esn=False):
+    def __init__(self, spi, alg, key, auth_key=b"", esn=False, mlen=None):
         self.spi = spi
         self.alg = alg
         self.key = bytes(key)          # GCM: cipher key || 4-byte salt (RFC 4106 8.1)
         self.auth_key = bytes(auth_key)
         self.esn = esn
+        # ICV bytes: xform_ah_authsize (GMAC 16, SHA1-HMAC 12); a GCM SA may
+        # carry a truncated 12- or 8-byte ICV (RFC 4106 s3.3, csp_auth_mlen)
+        self.mlen = mlen if mlen is not None else (16 if alg == GCM else 12)
 
     @property
     def ivlen(self):
@@ -36,7 +39,7 @@ class SecAssoc:
 
     @property
     def alen(self):
-        return 16 if self.alg == GCM else 12   # xform_ah_authsize: GMAC 16, SHA1-HMAC 12
+        return self.mlen
 
     @property
     def blocksize(self):
@@ -52,7 +55,8 @@ class SecAssoc:
                 csp_mode=L.CSP_MODE_AEAD,
                 csp_flags=L.CSP_F_SEPARATE_AAD if self.esn else 0,
                 csp_ivlen=12, csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16,
-                csp_cipher_klen=len(self.key) - 4, csp_cipher_key=self.key[:-4])
+                csp_cipher_klen=len(self.key) - 4, csp_cipher_key=self.key[:-4],
+                csp_auth_mlen=0 if self.mlen == 16 else self.mlen)
         return crypto_session_params(
             csp_mode=L.CSP_MODE_ETA, csp_flags=L.CSP_F_ESN if self.esn else 0,
             csp_ivlen=16, csp_cipher_alg=L.CRYPTO_AES_CBC, csp_cipher_klen=len(self.key),

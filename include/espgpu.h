@@ -47,10 +47,26 @@ extern "C" {
 #define ESPGPU_CRYPTO_HINT_MORE     0x1      /* cryptodev.h:612 */
 #define ESPGPU_PROBE_HARDWARE       (-100)   /* CRYPTODEV_PROBE_HARDWARE, cryptodev.h:345 */
 
-/* Status byte values written per record by the device (errno values). */
+/*
+ * Error codes returned by every entry point and written as the per-record
+ * status byte.  They are this ABI's own numbers (they coincide with Linux
+ * errno, the host the library runs on), NOT FreeBSD kernel errno: a
+ * kernel-domain shim translates them before they reach opencrypto, e.g.
+ * ESPGPU_EBADMSG -> EBADMSG (89), ESPGPU_ERESTART -> ERESTART (-1),
+ * ESPGPU_EAGAIN -> EAGAIN (35); see integration/ff_gpucrypto.c
+ * gpucrypto_errno().
+ */
 #define ESPGPU_OK       0
-#define ESPGPU_EINVAL   22
-#define ESPGPU_EBADMSG  74
+#define ESPGPU_ENOENT   2     /* unknown tuning key                            */
+#define ESPGPU_EIO      5     /* HIP runtime failure (espgpu_last_error says)  */
+#define ESPGPU_ENXIO    6
+#define ESPGPU_EAGAIN   11
+#define ESPGPU_ENOMEM   12    /* SA table full / allocation failure            */
+#define ESPGPU_ENODEV   19    /* no HIP device                                 */
+#define ESPGPU_EINVAL   22    /* malformed request or unsupported parameters   */
+#define ESPGPU_EBADMSG  74    /* ICV mismatch (status byte / crp_etype)        */
+#define ESPGPU_ERESTART 85    /* process(): staging full, requeue (cc_qblocked) */
+#define ESPGPU_ENOTSUP  95
 
 /* Mirror of struct crypto_session_params (cryptodev.h:357-384). */
 struct espgpu_session_params {

@@ -10,9 +10,11 @@
  *
  * Built here against include/espgpu.h and f-stack_amd/libespgpu.so by
  * `make -C integration` (tests/test_integration.py), so the binding a
- * maintainer adds is compile- and link-checked.
+ * maintainer adds is compile- and link-checked, and with the kernel-domain
+ * driver (ff_gpucrypto.c over integration/kmock) into kmock_gpu_test, which
+ * runs the whole driver path on the GPU.  Return codes are libespgpu's ABI
+ * codes; ff_gpucrypto.c translates them to FreeBSD errno.
  */
-#include <errno.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -30,6 +32,14 @@ int ff_gpucrypto_host_init(int gpu)
 
 	c.device = gpu;
 	return espgpu_init(&c, &g_ctx);
+}
+
+/* as ff_gpucrypto_host_init, with explicit staging sizes (batch_records,
+ * batch_bytes, nbatches: how much a burst may stage before process() answers
+ * ERESTART) */
+int ff_gpucrypto_host_configure(const struct espgpu_config *c)
+{
+	return espgpu_init(c, &g_ctx);
 }
 
 void ff_gpucrypto_host_fini(void)
@@ -50,7 +60,7 @@ int ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
 
 int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid)
 {
-	return g_ctx ? espgpu_newsession(g_ctx, csp, sid) : ENXIO;
+	return g_ctx ? espgpu_newsession(g_ctx, csp, sid) : ESPGPU_ENXIO;
 }
 
 void ff_gpucrypto_host_freesession(int32_t sid)
@@ -59,10 +69,11 @@ void ff_gpucrypto_host_freesession(int32_t sid)
 		espgpu_freesession(g_ctx, sid);
 }
 
-/* CRYPTODEV_PROCESS: 0 or ERESTART (the framework requeues) */
+/* CRYPTODEV_PROCESS: ESPGPU_OK or ESPGPU_ERESTART (the driver returns
+ * ERESTART and the framework requeues); the driver maps any other code */
 int ff_gpucrypto_host_process(const struct espgpu_req *r, int hint)
 {
-	return g_ctx ? espgpu_process(g_ctx, r, hint) : ENXIO;
+	return g_ctx ? espgpu_process(g_ctx, r, hint) : ESPGPU_ENXIO;
 }
 
 /* main_loop hook: launch the burst's staged records, deliver completions */

@@ -802,7 +802,10 @@ static int esp_process(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi
 	uint8_t aadbuf[12];
 	int gcm = (sa->mode == OREF_CSP_MODE_AEAD);
 	int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen;
-	int alen = gcm ? 16 : 12;                       /* xform_ah_authsize */
+	/* ICV bytes = the session's sw_mlen (cryptosoft.c:1112-1117): 16 for GCM
+	 * and 12 for HMAC-SHA1-96 as ESP sets them up (xform_ah_authsize), 8/12
+	 * for a truncated GCM session, 20 for an untruncated HMAC-SHA1 one */
+	int alen = sa->mlen;
 	int plen = len - hlen - alen;
 
 	if ((len & 3) || plen <= 0 || (!gcm && (plen & 15)))   /* :279-324 */

@@ -19,12 +19,13 @@ DESC = np.dtype([("off4", "<u4"), ("len", "<u2"), ("sa", "<u2"), ("esn_hi", "<u4
 
 
 class GcmSA:
-    def __init__(self, rng, klen=16, esn=False, spi=None):
+    def __init__(self, rng, klen=16, esn=False, spi=None, mlen=16):
         self.key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
         self.salt = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
         self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
         self.esn = esn
-        self.oracle = O.SA(O.CSP_MODE_AEAD, self.key, self.salt,
+        self.mlen = mlen                # ICV bytes: 16, or 12 / 8 truncated (RFC 4106 s3.3)
+        self.oracle = O.SA(O.CSP_MODE_AEAD, self.key, self.salt, mlen=mlen,
                            flags=O.CSP_F_SEPARATE_AAD if esn else 0)
 
 
@@ -35,6 +36,7 @@ class EtaSA:
         self.salt = b"\0\0\0\0"
         self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
         self.esn = esn
+        self.mlen = 12                  # HMAC-SHA1-96
         self.oracle = O.SA(O.CSP_MODE_ETA, self.key, akey=self.akey, mlen=12,
                            flags=O.CSP_F_ESN if esn else 0)
 
@@ -49,8 +51,8 @@ def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None
     """
     n = len(sa_idx)
     hlen = 16 if gcm else 24
-    alen = 16 if gcm else 12
-    lens = np.array([hlen + int(c) + alen for c in ct_lens], dtype=np.int64)
+    alens = np.array([sas[s].mlen for s in sa_idx], dtype=np.int64)
+    lens = np.array([hlen + int(c) + int(a) for c, a in zip(ct_lens, alens)], dtype=np.int64)
     offs = np.zeros(n, dtype=np.int64)
     pos = 0
     for i in range(n):
@@ -62,7 +64,7 @@ def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None
     payload = rng.integers(0, 256, pos + 64, dtype=np.uint8)
     for i in range(n):
         sa = sas[sa_idx[i]]
-        o, L = offs[i], lens[i]
+        o, L, alen = offs[i], lens[i], alens[i]
         rec = arena[o:o + L]
         rec[:] = payload[o:o + L]
         rec[0:4] = np.frombuffer(sa.spi.to_bytes(4, "big"), dtype=np.uint8)

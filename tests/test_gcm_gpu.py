@@ -30,10 +30,12 @@ def fw(drv):
 
 
 def payload_mask(descs, size, hlen=16, alen=16):
+    """alen: ICV bytes, one int or one per record."""
     m = np.zeros(size, dtype=bool)
-    for o4, L in zip(descs["off4"], descs["len"]):
+    alens = np.broadcast_to(np.asarray(alen), (len(descs),))
+    for o4, L, a in zip(descs["off4"], descs["len"], alens):
         o = int(o4) * 4
-        m[o + hlen:o + int(L) - alen] = True
+        m[o + hlen:o + int(L) - int(a)] = True
     return m
 
 
@@ -131,7 +133,7 @@ def _sessions(drv, sas):
     from espgpu.esp import GCM, SecAssoc
     sids = []
     for s in sas:
-        rc, sid = drv.newsession(SecAssoc(s.spi, GCM, s.key + s.salt, esn=s.esn).csp())
+        rc, sid = drv.newsession(SecAssoc(s.spi, GCM, s.key + s.salt, esn=s.esn, mlen=s.mlen).csp())
         assert rc == 0
         sids.append(sid)
     return sids
@@ -388,3 +390,128 @@ def test_kernel_grids_vs_oracle(drv, grid):
         drv.lib.espgpu_set_tuning(drv.ctx, b"grid", 0)
         for s in sids:
             drv.freesession(s)
+
+
+# ---------------------------------------------------------------------------
+# truncated ICVs (csp_auth_mlen 12 / 8: cryptosoft.c:1112-1117 keeps sw_mlen
+# bytes of the tag and compares that many, swcr_gcm :598-600, :636)
+
+@pytest.mark.parametrize("mlen", [12, 8])
+def test_truncated_icv_batch_vs_oracle(drv, mlen):
+    """Decrypt (out of place and verify-first in place) and encrypt with
+    truncated-ICV sessions mixed with a full-ICV one through the planner."""
+    from espgpu.batch import decrypt_batch, encrypt_batch
+    rng = np.random.default_rng(800 + mlen)
+    sas = [GcmSA(rng, 16, mlen=mlen), GcmSA(rng, 32, esn=True, mlen=mlen), GcmSA(rng, 16)]
+    sids = _sessions(drv, sas)
+    n = 1500
+    sa_idx = rng.integers(0, 3, n)
+    cts = rng.choice([4, 12, 204, 1448, 8948], n)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts,
+                                         esn_hi=rng.integers(0, 2**32, n, dtype=np.uint32))
+    alens = np.array([sas[i].mlen for i in sa_idx])
+    bad = ct.copy()
+    flip = rng.random(n) < 0.05
+    for i in np.nonzero(flip)[0]:       # a bit inside the (truncated) ICV
+        bad[int(descs["off4"][i]) * 4 + int(descs["len"][i]) - 1 - int(rng.integers(0, alens[i]))] ^= 0x02
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    for inplace in (False, True):
+        arena = _dev(bad)
+        out = arena if inplace else torch.zeros_like(arena)
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out)
+        torch.cuda.synchronize()
+        got = st.cpu().numpy()
+        assert (got == ref_st).all(), (inplace, np.nonzero(got != ref_st)[0][:10])
+        m = payload_mask(descs[~flip], len(bad), alen=alens[~flip])
+        assert (out.cpu().numpy()[m] == plain[m]).all()
+    arena = _dev(plain)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, _descs_dev(d), n, st)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert (arena.cpu().numpy() == ct).all()        # CT and the mlen-byte ICVs
+    for s in sids:
+        drv.freesession(s)
+
+
+@pytest.mark.parametrize("mlen", [12, 8])
+def test_truncated_icv_opencrypto(fw, mlen):
+    """esp_output -> esp_input through the driver path with a truncated-ICV
+    session: ciphertext and ICV bit-exact vs the oracle, a flipped ICV bit is
+    EBADMSG with the buffer untouched."""
+    from espgpu.esp import GCM, SecAssoc, esp_input_crp, esp_output_crp, esp_pad
+    rng = np.random.default_rng(900 + mlen)
+    key = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+    sa = SecAssoc(0x3000 + mlen, GCM, key, mlen=mlen)
+    err, ses = fw.crypto_newsession(sa.csp())
+    assert err == 0
+    orc = O.SA(O.CSP_MODE_AEAD, key[:-4], key[-4:], mlen=mlen)
+    pkts, refs = [], []
+    for nbytes in (20, 61, 1400, 8900):
+        body = esp_pad(rng.integers(0, 256, nbytes, dtype=np.uint8).tobytes())
+        rec = (sa.spi.to_bytes(4, "big") + (9).to_bytes(4, "big") +
+               rng.integers(0, 256, 8, dtype=np.uint8).tobytes() + body + bytes(mlen))
+        pkt = bytearray(bytes(20) + rec)
+        e, ref = orc.esp_encrypt(rec)
+        assert e == 0
+        pkts.append(pkt)
+        refs.append((rec, ref))
+        assert fw.crypto_dispatch(esp_output_crp(fw, ses, sa, pkt, 20)) == 0
+    fw.crypto_drain()
+    for pkt, (rec, ref) in zip(pkts, refs):
+        assert bytes(pkt[20:]) == ref
+    crps = [esp_input_crp(fw, ses, sa, pkt, 20) for pkt in pkts]
+    bad = bytearray(pkts[1])
+    bad[-1] ^= 0x80
+    before = bytes(bad)
+    crps.append(esp_input_crp(fw, ses, sa, bad, 20))
+    for c in crps:
+        assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+    for c, pkt, (rec, ref) in zip(crps, pkts, refs):
+        assert c.crp_etype == 0
+        assert bytes(pkt[20 + 16:-mlen]) == rec[16:-mlen]
+    assert crps[-1].crp_etype == O.EBADMSG and bytes(bad) == before
+    fw.crypto_freesession(ses)
+
+
+def test_two_streams_one_ctx(drv):
+    """One ctx used from two streams back to back (no host sync between):
+    the ctx's work-queue counters and planner workspace are shared, so the
+    second launch must be ordered after the first (run_batch waits on the
+    ctx's last-launch event); both batches come out bit-exact."""
+    from espgpu.batch import decrypt_batch
+    rng = np.random.default_rng(77)
+    sas = [GcmSA(rng, 16), GcmSA(rng, 32)]
+    sids = _sessions(drv, sas)
+    jobs = []
+    for k in range(2):
+        n = 3000 + 500 * k
+        sa_idx = rng.integers(0, 2, n)
+        plain, ct, descs, eh = build_records(rng, sas, sa_idx, rng.choice([12, 204, 1448, 8948], n))
+        d = descs.copy()
+        d["sa"] = [sids[s] for s in sa_idx]
+        jobs.append((n, plain, ct, descs, _descs_dev(d)))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(4):
+        outs = []
+        for (n, plain, ct, descs, ddev), s in zip(jobs, streams):
+            with torch.cuda.stream(s):
+                arena = _dev(ct)
+                out = torch.zeros_like(arena)
+                st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+            s.synchronize()
+            outs.append((arena, out, st))
+        for (n, plain, ct, descs, ddev), s, (arena, out, st) in zip(jobs, streams, outs):
+            decrypt_batch(drv, arena, ddev, n, st, out=out, grouped=False, stream=s)
+        torch.cuda.synchronize()
+        for (n, plain, ct, descs, ddev), (arena, out, st) in zip(jobs, outs):
+            assert (st.cpu().numpy() == 0).all(), rep
+            m = payload_mask(descs, len(ct))
+            assert (out.cpu().numpy()[m] == plain[m]).all(), rep
+    for s in sids:
+        drv.freesession(s)

@@ -154,3 +154,41 @@ def test_oracle_matches_reference_primitives_composed_as_swcr_gcm():
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["outputs_identical"] and res["tag_failures"] > 0
     assert 0.85 < res["ratio_oracle_over_ref"] < 1.15, res
+
+
+@pytest.mark.parametrize("mlen", [12, 8])
+def test_gcm_truncated_icv_kat(mlen):
+    """Truncated ICVs (csp_auth_mlen, cryptosoft.c:1112-1117): verification
+    compares the first mlen bytes of the DPDK KAT tag only (swcr_gcm :598-600)."""
+    for v in golden("gcm_aead.json")[:4]:
+        key, iv, ct = bytes.fromhex(v["key"]), bytes.fromhex(v["iv"]), bytes.fromhex(v["ciphertext"])
+        tag = bytes.fromhex(v["tag"])
+        e, pt, _ = O.gcm(key, iv, _aad(v), ct, tag[:mlen] + bytes(16 - mlen), mlen=mlen, encrypt=False)
+        assert e == 0 and pt.hex() == v["plaintext"]
+        wrong = bytearray(tag)
+        wrong[mlen - 1] ^= 0x01
+        e, _, _ = O.gcm(key, iv, _aad(v), ct, bytes(wrong), mlen=mlen, encrypt=False)
+        assert e == O.EBADMSG
+
+
+@pytest.mark.parametrize("mlen", [12, 8])
+def test_esp_truncated_icv_is_tag_prefix(mlen):
+    """An ESP record under a truncated-ICV SA is the full-ICV record with the
+    ICV cut to its first mlen bytes; decrypt verifies it, a flip fails it."""
+    rng = np.random.default_rng(40 + mlen)
+    key, salt = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), b"\x01\x02\x03\x04"
+    full = O.SA(O.CSP_MODE_AEAD, key, salt)
+    trunc = O.SA(O.CSP_MODE_AEAD, key, salt, mlen=mlen)
+    for ct_len in (4, 12, 100, 1448):
+        body = rng.integers(0, 256, 16 + ct_len, dtype=np.uint8).tobytes()
+        e, r16 = full.esp_encrypt(body + bytes(16))
+        assert e == 0
+        e, rm = trunc.esp_encrypt(body + bytes(mlen))
+        assert e == 0
+        assert rm[:-mlen] == r16[:-16] and rm[-mlen:] == r16[-16:-16 + mlen]
+        e, dec = trunc.esp_decrypt(rm)
+        assert e == 0 and dec[16:-mlen] == body[16:]
+        bad = bytearray(rm)
+        bad[-1] ^= 0x04
+        e, out = trunc.esp_decrypt(bytes(bad))
+        assert e == O.EBADMSG and out == bytes(bad)
