@@ -22,6 +22,8 @@
 //  * CBC encryption is serial per record (lane = record), Te0/Te1 in LDS.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "espgpu_internal.h"
 
 namespace espgpu {
@@ -403,6 +405,11 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
+  // implicit units (64 records, one wave each): no more workgroups than units
+  if (p.chunks == nullptr) {
+    const int units = (int)((p.n + 63) / 64), wpg = (encrypt ? 1024 : 768) / 64;
+    grid = std::max(1, std::min(grid, (units + wpg - 1) / wpg));
+  }
   const int two_pass = !encrypt && p.out == p.arena;
   if (encrypt)
     hipLaunchKernelGGL((eta_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, p);

@@ -41,6 +41,8 @@
 //    record + descriptor + plaintext + status byte.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "espgpu_internal.h"
 
 namespace espgpu {
@@ -650,6 +652,9 @@ int set_gcm_opts(uint32_t opts) {
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
+  // implicit chunks: no more workgroups than chunks (a 32-record burst is one
+  // chunk: one workgroup instead of 256 that only fill LDS and leave)
+  if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + kChunkRecs - 1) / kChunkRecs)));
   if (encrypt)
     hipLaunchKernelGGL((gcm_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, p);
   else if (two_pass)

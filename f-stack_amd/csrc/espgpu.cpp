@@ -27,6 +27,9 @@ using namespace espgpu;
 
 namespace {
 
+// flush(): batches up to this many staged bytes run on one stream (latency)
+constexpr uint32_t kSmallBatchBytes = 128u << 10;
+
 struct Session {
   bool used = false;
   int mode = 0, flags = 0, mlen = 0, klen = 0;
@@ -47,16 +50,25 @@ struct Pending {
 
 enum { SLOT_FREE = 0, SLOT_FILLING = 1, SLOT_INFLIGHT = 2 };
 
+// A staging slot.  One pinned host buffer and its device mirror(s) hold, at
+// flush time, [records: bytes][16 B slack][descriptors: nrec*16][status: nrec],
+// so a batch is ONE H2D copy, the kernel(s), and ONE D2H copy (records and
+// status together) -- what bounds a 32-record burst's latency is the number of
+// queue operations, not bytes.
 struct Slot {
   int state = SLOT_FREE;
   int op = -1;                // 0 decrypt, 1 encrypt
   uint8_t *h_arena = nullptr, *d_arena = nullptr, *d_out = nullptr;
-  espgpu_desc *h_desc = nullptr, *d_desc = nullptr;
-  uint8_t *h_status = nullptr, *d_status = nullptr;
+  espgpu_desc *h_desc = nullptr;            // descriptors while filling
   uint32_t nrec = 0, bytes = 0;
+  uint32_t desc_off = 0, stat_off = 0;      // set by flush
+  int32_t sid0 = -1;                        // session of the first record
+  bool mixed = false;                       // more than one session staged
+  uint32_t kinds = 0;                       // 1: GCM records, 2: ETA records
   std::vector<Pending> reqs;             // reserved to batch_records: no per-record allocation
   std::vector<espgpu_seg> segpool;       // segment lists of the staged requests
   hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
+  hipStream_t st = nullptr;                 // small batches: copy, kernel, copy in order here
 };
 
 }  // namespace
@@ -173,34 +185,40 @@ bool seg_copy_in(const espgpu_seg *segs, uint32_t nsegs, uint32_t off, uint32_t 
 }
 
 int alloc_slot(espgpu_ctx *c, Slot &s) {
-  const size_t bytes = c->cfg.batch_bytes + 64, recs = c->cfg.batch_records;
+  const size_t recs = c->cfg.batch_records;
+  const size_t bytes = c->cfg.batch_bytes + 64 + recs * (sizeof(espgpu_desc) + 1) + 64;
   HIPCHK(c, hipHostMalloc((void **)&s.h_arena, bytes, hipHostMallocDefault));
-  HIPCHK(c, hipHostMalloc((void **)&s.h_desc, recs * sizeof(espgpu_desc), hipHostMallocDefault));
-  HIPCHK(c, hipHostMalloc((void **)&s.h_status, recs, hipHostMallocDefault));
+  s.h_desc = new espgpu_desc[recs];
   HIPCHK(c, hipMalloc(&s.d_arena, bytes));
   HIPCHK(c, hipMalloc(&s.d_out, bytes));
-  HIPCHK(c, hipMalloc(&s.d_desc, recs * sizeof(espgpu_desc)));
-  HIPCHK(c, hipMalloc(&s.d_status, recs));
   HIPCHK(c, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   HIPCHK(c, hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming));
   HIPCHK(c, hipEventCreate(&s.k0));
   HIPCHK(c, hipEventCreate(&s.k1));
+  HIPCHK(c, hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
   s.reqs.reserve(recs);
   s.segpool.reserve(recs * 2);
   return 0;
 }
 
 void free_slot(Slot &s) {
-  hipHostFree(s.h_arena); hipHostFree(s.h_desc); hipHostFree(s.h_status);
-  hipFree(s.d_arena); hipFree(s.d_out); hipFree(s.d_desc); hipFree(s.d_status);
+  hipHostFree(s.h_arena);
+  delete[] s.h_desc;
+  hipFree(s.d_arena); hipFree(s.d_out);
   for (hipEvent_t e : {s.done, s.in_done, s.k0, s.k1})
     if (e) hipEventDestroy(e);
+  if (s.st) {
+    hipStreamSynchronize(s.st);
+    hipStreamDestroy(s.st);
+  }
 }
 
 // Launch the crypto kernels for one batch of device-resident records.
+// kinds: which kernels the batch needs (1 GCM, 2 ETA); the device-resident
+// entry points do not know and pass both.
 int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
               uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st,
-              uint32_t *d_trailer = nullptr) {
+              uint32_t *d_trailer = nullptr, uint32_t kinds = 3) {
   if (n == 0) return 0;
   if (c->launched && st != c->last_st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
   const uint32_t nsas = (uint32_t)c->sessions.size();
@@ -227,8 +245,9 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  if (launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
-  if (c->n_eta > 0) {
+  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st))
+    return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
+  if ((kinds & 2) && c->n_eta > 0) {
     EtaParams q{};
     q.arena = d_arena;
     q.out = p.out;
@@ -442,6 +461,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   espgpu_flush(c);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
+  for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
   if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
   c->sessions[sid] = Session();
   DevSA z;
@@ -520,6 +540,9 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
     s->bytes = 0;
     s->reqs.clear();
     s->segpool.clear();
+    s->sid0 = sid;
+    s->mixed = false;
+    s->kinds = 0;
   }
   Pending pd;
   pd.opaque = r->opaque;
@@ -555,6 +578,8 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   d.salt = salt;
   s->bytes += (rlen + 15) & ~15u;
   s->nrec++;
+  s->mixed |= (sid != s->sid0);
+  s->kinds |= gcm ? 1u : 2u;
   s->reqs.push_back(pd);
   return 0;
 }
@@ -563,20 +588,39 @@ int espgpu_flush(espgpu_ctx *c) {
   if (!c) return ESPGPU_EINVAL;
   Slot &s = c->slots[c->cur];
   if (s.state != SLOT_FILLING || s.nrec == 0) return 0;
-  // H2D on s_in -> kernels on the compute stream -> D2H on s_out, chained by
-  // events, so consecutive batches overlap their copies with each other's kernels.
-  HIPCHK(c, hipMemcpyAsync(s.d_arena, s.h_arena, s.bytes + 16, hipMemcpyHostToDevice, c->s_in));
-  HIPCHK(c, hipMemcpyAsync(s.d_desc, s.h_desc, s.nrec * sizeof(espgpu_desc), hipMemcpyHostToDevice, c->s_in));
-  HIPCHK(c, hipEventRecord(s.in_done, c->s_in));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, s.in_done, 0));
-  hipEventRecord(s.k0, c->stream);
-  int e = run_batch(c, s.d_arena, s.d_desc, s.nrec, s.d_status, s.op ? nullptr : s.d_out, 0, s.op, c->stream);
+  // [records][16 B slack][descriptors][status]: one H2D on s_in -> kernels on
+  // the compute stream -> one D2H on s_out, chained by events, so consecutive
+  // batches overlap their copies with each other's kernels.
+  s.desc_off = s.bytes + 16;
+  s.stat_off = s.desc_off + s.nrec * (uint32_t)sizeof(espgpu_desc);
+  memset(s.h_arena + s.bytes, 0, 16);
+  memcpy(s.h_arena + s.desc_off, s.h_desc, s.nrec * sizeof(espgpu_desc));
+  // A small batch (an RX burst) runs copy, kernel, copy in order on its
+  // slot's own stream: cross-stream event hand-offs cost more latency than
+  // the copies; the next slot's burst overlaps on the other slot's stream
+  // (kernels stay ordered through run_batch's last-launch event).  Large
+  // batches use the three ctx streams so batch k+1's H2D overlaps batch k's
+  // kernels and batch k-1's D2H.
+  const bool small = s.stat_off <= kSmallBatchBytes;
+  hipStream_t s_k = small ? s.st : c->stream;
+  hipStream_t s_in = small ? s.st : c->s_in, s_out = small ? s.st : c->s_out;
+  HIPCHK(c, hipMemcpyAsync(s.d_arena, s.h_arena, s.stat_off, hipMemcpyHostToDevice, s_in));
+  if (!small) {
+    HIPCHK(c, hipEventRecord(s.in_done, s_in));
+    HIPCHK(c, hipStreamWaitEvent(s_k, s.in_done, 0));
+  }
+  hipEventRecord(s.k0, s_k);
+  uint8_t *dres = s.op ? s.d_arena : s.d_out;      // records out: in place (encrypt) or d_out
+  // a single-session batch skips the device planner (ESPGPU_BATCH_GROUPED:
+  // one session trivially satisfies "one session per chunk")
+  int e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
+                    dres + s.stat_off, s.op ? nullptr : s.d_out, s.mixed ? 0u : (uint32_t)ESPGPU_BATCH_GROUPED,
+                    s.op, s_k, nullptr, s.kinds);
   if (e) return e;
-  hipEventRecord(s.k1, c->stream);
-  HIPCHK(c, hipStreamWaitEvent(c->s_out, s.k1, 0));
-  HIPCHK(c, hipMemcpyAsync(s.h_arena, s.op ? s.d_arena : s.d_out, s.bytes, hipMemcpyDeviceToHost, c->s_out));
-  HIPCHK(c, hipMemcpyAsync(s.h_status, s.d_status, s.nrec, hipMemcpyDeviceToHost, c->s_out));
-  HIPCHK(c, hipEventRecord(s.done, c->s_out));
+  hipEventRecord(s.k1, s_k);
+  if (!small) HIPCHK(c, hipStreamWaitEvent(s_out, s.k1, 0));
+  HIPCHK(c, hipMemcpyAsync(s.h_arena, dres, s.stat_off + s.nrec, hipMemcpyDeviceToHost, s_out));
+  HIPCHK(c, hipEventRecord(s.done, s_out));
   s.state = SLOT_INFLIGHT;
   c->stats.batches++;
   c->cur = (c->cur + 1) % (int)c->slots.size();
@@ -590,7 +634,7 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
     c->stats.kernel_ns += (uint64_t)(ms * 1e6);
   }
   for (auto &pd : s.reqs) {
-    int et = pd.etype_pre >= 0 ? pd.etype_pre : (int)s.h_status[pd.rec];
+    int et = pd.etype_pre >= 0 ? pd.etype_pre : (int)s.h_arena[s.stat_off + pd.rec];
     if (et == 0) {
       const uint8_t *src = s.h_arena + pd.stage_off;
       for (int k = 0; k < pd.nspan; ++k)
@@ -637,9 +681,13 @@ int espgpu_drain(espgpu_ctx *c) {
   if (!c) return ESPGPU_EINVAL;
   int e = espgpu_flush(c);
   if (e) return e;
-  HIPCHK(c, hipStreamSynchronize(c->s_out));
-  for (auto &s : c->slots)
-    if (s.state == SLOT_INFLIGHT) complete_slot(c, s);
+  // oldest first (slot cur is the next to fill, so cur+1.. are older batches)
+  for (size_t k = 0; k < c->slots.size(); ++k) {
+    Slot &s = c->slots[(c->cur + k) % c->slots.size()];
+    if (s.state != SLOT_INFLIGHT) continue;
+    HIPCHK(c, hipEventSynchronize(s.done));
+    complete_slot(c, s);
+  }
   return 0;
 }
 

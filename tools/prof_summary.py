@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run into profiles/<tag>.json (+ pmc_<cfg>.json).
 
-  python tools/prof_summary.py gpurun_out/prof_<tag> <tag> [cfg]
+  python tools/prof_summary.py gpurun_out/prof_<tag> <tag> [cfg] [--inplace]
 
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
@@ -27,6 +27,16 @@ def kernel_stats(d):
     return out
 
 
+def steady_durations(d, name, skip):
+    """Per-launch durations (ns) of kernel `name` from the kernel trace, in
+    dispatch order, without the first `skip` launches (the bench's untimed
+    warm-up launches, which include first-touch page mapping)."""
+    p = os.path.join(d, "trace", "run_kernel_trace.csv")
+    rows = [r for r in csv.DictReader(open(p)) if r["Kernel_Name"] == name]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    return [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows][skip:]
+
+
 def counters(d, sub, match):
     p = os.path.join(d, sub, "run_counter_collection.csv")
     if not os.path.exists(p):
@@ -39,15 +49,20 @@ def counters(d, sub, match):
 
 
 def main():
-    d, tag = sys.argv[1], sys.argv[2]
-    cfg = sys.argv[3] if len(sys.argv) > 3 else "cfg1"
+    argv = [a for a in sys.argv[1:] if a != "--inplace"]
+    inplace = "--inplace" in sys.argv
+    d, tag = argv[0], argv[1]
+    cfg = argv[2] if len(argv) > 2 else "cfg1"
     ks = kernel_stats(d)
     dominant = max(ks, key=lambda k: ks[k]["pct"])
-    key = "gcm_kernel<0>" if "gcm_kernel<0>" in dominant else dominant
+    key = dominant
     c = {}
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_sq3"):
         c.update(counters(d, sub, key))
-    res = {"tag": tag, "config": cfg, "dominant_kernel": dominant, "kernels": ks, "counters": c}
+    steady = steady_durations(d, dominant, 10)     # profile.sh runs bench.py --warmup 10
+    steady_ms = sum(steady) / len(steady) / 1e6 if steady else None
+    res = {"tag": tag, "config": cfg, "dominant_kernel": dominant, "kernels": ks, "counters": c,
+           "steady_avg_kernel_ms": steady_ms, "steady_launches": len(steady)}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         rd = 2 * c["FETCH_SIZE"] * 1024
         wr = c["WRITE_SIZE"] * 1024
@@ -60,8 +75,14 @@ def main():
     with open(os.path.join(ROOT, "profiles", "%s.json" % tag), "w") as f:
         json.dump(res, f, indent=1)
     if "hbm_bytes_per_launch" in res:
-        with open(os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg), "w") as f:
-            json.dump({"source": "profiles/%s.json" % tag,
+        # what bench.py reads: traffic is used only when dominant_kernel is the
+        # kernel the bench launches
+        with open(os.path.join(ROOT, "profiles", "pmc_%s%s.json" % (cfg, "_inplace" if inplace else "")),
+                  "w") as f:
+            json.dump({"source": "profiles/%s.json" % tag, "dominant_kernel": dominant,
+                       "avg_kernel_ms": round(steady_ms or ks[dominant]["avg_ns"] / 1e6, 4),
+                       "avg_kernel_ms_all_calls": round(ks[dominant]["avg_ns"] / 1e6, 4),
+                       "calls": ks[dominant]["calls"],
                        "hbm_bytes_per_launch": round(res["hbm_bytes_per_launch"])}, f, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
     print("dominant:", dominant, ks[dominant])
