@@ -8,17 +8,23 @@
 //   HMAC-SHA1 over AAD || payload (|| ESN high 32 bits, CSP_F_ESN), ICV = the
 //   first mlen (12) bytes, IV = the 16 bytes before the payload.
 //
-// Mapping: a wave owns 64 records.
+// Mapping: a wave owns 64 records (lane = record for everything serial).
 //  * HMAC-SHA1 is a serial chain per record, so lane = record: each lane runs
 //    its record's SHA-1 compressions from the precomputed ipad/opad chaining
 //    states (hmac_init_pad, crypto.c:413-441), 80 rounds fully unrolled in
 //    registers, no tables.
-//  * CBC decryption is block-parallel: the wave then walks its 64 records one
-//    at a time and all 64 lanes decrypt that record's blocks (P_i = D(C_i) ^
-//    C_{i-1}), 64 consecutive blocks per pass, last pass first, so in-place
-//    decryption never reads a block another lane already overwrote.  AES decryption uses Td0/Td1 tables replicated 32x in LDS
-//    (conflict-free ds_read_b32, one v_perm_b32 per address, as in esp_gcm.hip)
-//    and a replicated inverse S-box for the last round.
+//  * Out-of-place decrypt (MODE 0, the benchmarked path) is ONE pass per
+//    record (eta_decrypt_fused): every 64-byte HMAC chunk the lane loads also
+//    completes up to four CBC blocks, which it decrypts with four AES states
+//    in flight (aes_dec4) and stores, so the record is read once.
+//  * In-place verify-first decrypt (MODE 2) must authenticate before it may
+//    overwrite: HMAC pass first, then the CBC pass is block-parallel -- the
+//    wave walks its records as one flat block list, 64 consecutive blocks per
+//    pass (1 KiB contiguous per instruction), last pass first, so in-place
+//    decryption never reads a block another lane already overwrote.
+//  * AES decryption uses Td0/Td1 tables replicated 32x in LDS (conflict-free
+//    ds_read_b32, one v_perm_b32 per address, as in esp_gcm.hip) and a
+//    replicated inverse S-box for the last round.
 //  * CBC encryption is serial per record (lane = record), Te0/Te1 in LDS.
 #include <hip/hip_runtime.h>
 
@@ -114,6 +120,56 @@ __device__ __forceinline__ uint4 aes_dec(uint4 in, KP dk, int nr, const uint8_t 
     o[c] = (a | (b << 8) | (cc << 16) | (d << 24)) ^ bswap32(dk[4 * nr + c]);
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Four independent blocks through the same rounds: 64 table reads in flight
+// per lane per round instead of 16 (the decrypt of one 64-byte HMAC chunk).
+template <typename KP>
+__device__ __forceinline__ void aes_dec4(uint4 (&v)[4], KP dk, int nr, const uint8_t *lds, uint32_t slot) {
+  uint32_t s[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s[q][0] = bswap32(v[q].x) ^ dk[0];
+    s[q][1] = bswap32(v[q].y) ^ dk[1];
+    s[q][2] = bswap32(v[q].z) ^ dk[2];
+    s[q][3] = bswap32(v[q].w) ^ dk[3];
+  }
+#pragma unroll 1
+  for (int r = 1; r < nr; ++r) {
+    const uint32_t k0 = ror16(dk[4 * r]), k1 = ror16(dk[4 * r + 1]);
+    const uint32_t k2 = ror16(dk[4 * r + 2]), k3 = ror16(dk[4 * r + 3]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t s0 = s[q][0], s1 = s[q][1], s2 = s[q][2], s3 = s[q][3];
+      const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s3, slot, 2));
+      const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s1, slot, 0));
+      const uint32_t a1 = t0(lds, tpa(s1, slot, 3)), b1 = t1(lds, tpa(s0, slot, 2));
+      const uint32_t c1 = t0(lds, tpa(s3, slot, 1)), d1 = t1(lds, tpa(s2, slot, 0));
+      const uint32_t a2 = t0(lds, tpa(s2, slot, 3)), b2 = t1(lds, tpa(s1, slot, 2));
+      const uint32_t c2 = t0(lds, tpa(s0, slot, 1)), d2 = t1(lds, tpa(s3, slot, 0));
+      const uint32_t a3 = t0(lds, tpa(s3, slot, 3)), b3 = t1(lds, tpa(s2, slot, 2));
+      const uint32_t c3 = t0(lds, tpa(s1, slot, 1)), d3 = t1(lds, tpa(s0, slot, 0));
+      s[q][0] = xor3(a0, b0, ror16(xor3(c0, d0, k0)));
+      s[q][1] = xor3(a1, b1, ror16(xor3(c1, d1, k1)));
+      s[q][2] = xor3(a2, b2, ror16(xor3(c2, d2, k2)));
+      s[q][3] = xor3(a3, b3, ror16(xor3(c3, d3, k3)));
+    }
+  }
+  const uint32_t *si = reinterpret_cast<const uint32_t *>(lds + LDS_SI);
+  const uint32_t ls = slot >> 2;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t a = si[((s[q][c] >> 24) << 5) | ls];
+      const uint32_t b = si[(((s[q][(c + 3) & 3] >> 16) & 0xff) << 5) | ls];
+      const uint32_t cc = si[(((s[q][(c + 2) & 3] >> 8) & 0xff) << 5) | ls];
+      const uint32_t d = si[((s[q][(c + 1) & 3] & 0xff) << 5) | ls];
+      o[c] = (a | (b << 8) | (cc << 16) | (d << 24)) ^ bswap32(dk[4 * nr + c]);
+    }
+    v[q] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
 }
 
 // ---- AES encryption (rijndaelEncrypt) with Te0/Te1 in LDS ------------------
@@ -239,6 +295,132 @@ __device__ void hmac_sha1(const uint8_t *rec, uint32_t L0, bool esn, uint32_t es
 
 __device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
 
+// One pass over an ETA record for the out-of-place decrypt: the record is
+// read once, in 64-byte HMAC chunks (lane = record); each chunk feeds the
+// SHA-1 compression AND the CBC decryption of the CT blocks it completes, so
+// the ciphertext is not fetched a second time for the cipher.  ESP places CT
+// block i at 24 + 16i: chunk 0 holds the IV (C_-1) and blocks 0, 1; chunk
+// b >= 1 holds the 8-byte tail of block 4b-2 and blocks 4b-1 .. 4b+1, whose
+// other 8 bytes came at the end of chunk b-1 (carried in two registers).
+// The <= 4 blocks after the last full chunk are decrypted on the way through
+// the first partial chunk.  Writes plaintext to out (MODE 0 decrypts records
+// whose ICV fails too; the status byte says so, as in the GCM kernel).
+// Returns whether the first mlen bytes of the HMAC match the ICV; *trl gets
+// the esp_input_cb trailer word from the last block.
+__device__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *orec, uint32_t plen, uint32_t mlen, bool esn,
+                                  uint32_t esn_hi, kptr ipad, kptr opad, kptr dk, int nr, const uint8_t *lds,
+                                  uint32_t slot, bool act, uint32_t *trl) {
+  const uint32_t L0 = 24 + plen, L = L0 + (esn ? 4u : 0u);
+  const uint32_t nfull = L0 / 64, total = (L + 9 + 63) / 64, nblk = plen / 16;
+  const uint64_t bits = (uint64_t)(64 + L) * 8;
+  uint32_t T = act ? total : 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) T = max(T, (uint32_t)__shfl_xor((int)T, o));
+  uint32_t h[5] = {ipad[0], ipad[1], ipad[2], ipad[3], ipad[4]};
+  uint4 prev = make_uint4(0, 0, 0, 0);
+  uint32_t cy0 = 0, cy1 = 0;
+  for (uint32_t b = 0; b <= T; ++b) {
+    const bool on = act && b <= total;
+    uint32_t w[16];
+    uint32_t m[16];
+    if (on && b < nfull) {
+      const uint8_t *q = rec + 64 * b;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 v = ld16(q + 16 * k);
+        m[4 * k] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
+      }
+      uint4 blk[4];
+      int i0, nb;
+      if (b == 0) {                       // wave-uniform: every lane is at chunk 0 together
+        prev = make_uint4(m[2], m[3], m[4], m[5]);
+        blk[0] = make_uint4(m[6], m[7], m[8], m[9]);
+        blk[1] = make_uint4(m[10], m[11], m[12], m[13]);
+        blk[2] = blk[3] = make_uint4(0, 0, 0, 0);
+        i0 = 0;
+        nb = 2;
+      } else {
+        blk[0] = make_uint4(cy0, cy1, m[0], m[1]);
+        blk[1] = make_uint4(m[2], m[3], m[4], m[5]);
+        blk[2] = make_uint4(m[6], m[7], m[8], m[9]);
+        blk[3] = make_uint4(m[10], m[11], m[12], m[13]);
+        i0 = 4 * (int)b - 2;
+        nb = 4;
+      }
+      cy0 = m[14];
+      cy1 = m[15];
+      uint4 d[4] = {blk[0], blk[1], blk[2], blk[3]};
+      aes_dec4(d, dk, nr, lds, slot);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < nb) {
+          st16(orec + 24 + 16 * (i0 + k), xor4(d[k], prev));
+          prev = blk[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap32(m[k]);
+    } else if (on && b < total) {
+      if (b == nfull) {
+        // the CT blocks after the last full chunk (1..4 of them)
+        const int i0 = nfull == 0 ? 0 : 4 * (int)nfull - 2;
+        if (nfull == 0) prev = ld16(rec + 8);
+        uint4 blk[4], d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          blk[k] = make_uint4(0, 0, 0, 0);
+          if (i0 + k < (int)nblk) blk[k] = ld16(rec + 24 + 16 * (i0 + k));
+          d[k] = blk[k];
+        }
+        aes_dec4(d, dk, nr, lds, slot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (i0 + k < (int)nblk) {
+            const uint4 pt = xor4(d[k], prev);
+            st16(orec + 24 + 16 * (i0 + k), pt);
+            if (i0 + k == (int)nblk - 1) *trl = esp_trailer_word(pt.w, plen);
+            prev = blk[k];
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t o = 64 * b + 4 * k;
+        uint32_t v;
+        if (o + 4 <= L0) v = bswap32(*reinterpret_cast<const uint32_t *>(rec + o));
+        else if (esn && o == L0) v = esn_hi;
+        else if (o == L) v = 0x80000000u;
+        else v = 0;
+        if (b == total - 1 && k == 14) v = (uint32_t)(bits >> 32);
+        if (b == total - 1 && k == 15) v = (uint32_t)bits;
+        w[k] = v;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) w[k] = h[k];
+      w[5] = 0x80000000u;
+#pragma unroll
+      for (int k = 6; k < 15; ++k) w[k] = 0;
+      w[15] = (64 + 20) * 8;
+      if (on) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) h[k] = opad[k];
+      }
+    }
+    uint32_t hn[5] = {h[0], h[1], h[2], h[3], h[4]};
+    sha1_compress(hn, w);
+    if (on) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) h[k] = hn[k];
+    }
+  }
+  uint32_t diff = 0;
+  if (act)
+    for (uint32_t k = 0; k < mlen / 4; ++k)
+      diff |= bswap32(h[k]) ^ *reinterpret_cast<const uint32_t *>(rec + L0 + 4 * k);
+  return act && diff == 0;
+}
+
 // MODE 0: decrypt out-of-place; 1: encrypt in place; 2: decrypt in place (verify first)
 template <int MODE, int WG>
 __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
@@ -296,7 +478,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         const int pl = (int)len - 24 - (int)mlen;           // hlen 24, alen = mlen (12)
         valid = pl > 0 && (pl & 15) == 0 && (len & 3) == 0;  // xform_esp.c:316-324
         plen = valid ? (uint32_t)pl : 0;
-        if (valid && MODE != 1) {
+        if (valid && MODE == 2) {
           uint32_t dg[5];
           const uint8_t *rec = p.arena + off;
           hmac_sha1(rec, 24 + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, dv.z, kp(s->ipad),
@@ -327,6 +509,31 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           *reinterpret_cast<uint32_t *>(rec + 24 + plen + 4 * k) = bswap32(dg[k]);
       }
       if (have) p.status[di] = valid ? ESPGPU_OK : ESPGPU_EINVAL;
+      continue;
+    }
+    if (MODE == 0) {
+      // ---- out-of-place decrypt: one fused pass per record (lane = record),
+      // one session at a time so round keys and pads stay in SGPRs ----
+      bool run = have && valid;
+      uint64_t todo = __ballot(run);
+      while (todo) {
+        const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
+        const bool mine = run && sa == sau;
+        todo &= ~__ballot(mine);
+        run = run && !mine;
+        const DevSA *s = p.sas + sau;
+        uint32_t trl = 0;
+        const bool good = eta_decrypt_fused(p.arena + off, p.out + off, plen, s->mlen,
+                                            (s->flags & ESPGPU_CSP_F_ESN) != 0, mine ? p.desc[di].esn_hi : 0,
+                                            kp(s->ipad), kp(s->opad), kp(s->dk), (int)s->nr, lds, slot, mine,
+                                            &trl);
+        if (mine) {
+          ok = good;
+          if (p.trailer) p.trailer[di] = good ? trl : 0u;
+        }
+      }
+      if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+      if (have && p.trailer && !valid) p.trailer[di] = 0;
       continue;
     }
     if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
