@@ -593,10 +593,177 @@ void oref_hmac_sha1(const uint8_t *key, int klen, const uint8_t *msg, size_t len
 }
 
 /* ------------------------------------------------------------------------ */
+/* SHA-256 (freebsd/crypto/sha2/sha256c.c: K[] :83, SHA256_Transform :135,   */
+/* SHA256_Init :229) in the same context shape as SHA-1 above                 */
+
+static const uint32_t SHA256_K[64] = {
+	0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+	0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+	0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+	0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+	0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+	0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+	0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+	0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2,
+};
+
+static void sha256_block(uint32_t h[8], const uint8_t *m)
+{
+	uint32_t w[64], v[8];
+
+	for (int t = 0; t < 16; t++)
+		w[t] = ld_be32(m + 4 * t);
+	for (int t = 16; t < 64; t++) {
+		uint32_t s0 = ror32(w[t - 15], 7) ^ ror32(w[t - 15], 18) ^ (w[t - 15] >> 3);
+		uint32_t s1 = ror32(w[t - 2], 17) ^ ror32(w[t - 2], 19) ^ (w[t - 2] >> 10);
+		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+	}
+	memcpy(v, h, sizeof(v));
+	for (int t = 0; t < 64; t++) {
+		uint32_t S1 = ror32(v[4], 6) ^ ror32(v[4], 11) ^ ror32(v[4], 25);
+		uint32_t ch = (v[4] & v[5]) ^ (~v[4] & v[6]);
+		uint32_t t1 = v[7] + S1 + ch + SHA256_K[t] + w[t];
+		uint32_t S0 = ror32(v[0], 2) ^ ror32(v[0], 13) ^ ror32(v[0], 22);
+		uint32_t maj = (v[0] & v[1]) ^ (v[0] & v[2]) ^ (v[1] & v[2]);
+		uint32_t t2 = S0 + maj;
+		v[7] = v[6]; v[6] = v[5]; v[5] = v[4]; v[4] = v[3] + t1;
+		v[3] = v[2]; v[2] = v[1]; v[1] = v[0]; v[0] = t1 + t2;
+	}
+	for (int i = 0; i < 8; i++)
+		h[i] += v[i];
+}
+
+/* A hash context for either auth algorithm of an ETA session. */
+struct hctx {
+	int alg;                /* OREF_CRYPTO_SHA1_HMAC or OREF_CRYPTO_SHA2_256_HMAC */
+	uint32_t h[8];
+	uint64_t nbytes;
+	uint8_t buf[64];
+	unsigned fill;
+};
+
+static int hash_len(int alg) { return alg == OREF_CRYPTO_SHA2_256_HMAC ? 32 : 20; }
+
+static void h_init(struct hctx *c, int alg)
+{
+	static const uint32_t iv256[8] = { 0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+	    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19 };
+	struct sha1_ctx s1;
+
+	memset(c, 0, sizeof(*c));
+	c->alg = alg;
+	if (alg == OREF_CRYPTO_SHA2_256_HMAC) {
+		memcpy(c->h, iv256, sizeof(iv256));
+	} else {
+		sha1_init(&s1);
+		memcpy(c->h, s1.h, sizeof(s1.h));
+	}
+}
+
+static void h_block(struct hctx *c, const uint8_t *m)
+{
+	if (c->alg == OREF_CRYPTO_SHA2_256_HMAC)
+		sha256_block(c->h, m);
+	else
+		sha1_block(c->h, m);
+}
+
+static void h_update(struct hctx *c, const uint8_t *p, size_t n)
+{
+	c->nbytes += n;
+	while (n > 0) {
+		size_t k = 64 - c->fill;
+		if (k > n)
+			k = n;
+		memcpy(c->buf + c->fill, p, k);
+		c->fill += (unsigned)k;
+		p += k;
+		n -= k;
+		if (c->fill == 64) {
+			h_block(c, c->buf);
+			c->fill = 0;
+		}
+	}
+}
+
+static void h_final(uint8_t *out, struct hctx *c)
+{
+	uint64_t bits = c->nbytes * 8;
+	uint8_t pad = 0x80, z = 0, lb[8];
+
+	h_update(c, &pad, 1);
+	while (c->fill != 56)
+		h_update(c, &z, 1);
+	st_be64(lb, bits);
+	h_update(c, lb, 8);
+	for (int i = 0; i < hash_len(c->alg) / 4; i++)
+		st_be32(out + 4 * i, c->h[i]);
+}
+
+void oref_sha256(const uint8_t *msg, size_t len, uint8_t out[32])
+{
+	struct hctx c;
+
+	h_init(&c, OREF_CRYPTO_SHA2_256_HMAC);
+	h_update(&c, msg, len);
+	h_final(out, &c);
+}
+
+/* hmac_init_pad (crypto.c:413-441) for either hash */
+static void h_hmac_pad(const uint8_t *key, int klen, struct hctx *c, int alg, uint8_t padval)
+{
+	uint8_t k[64];
+
+	memset(k, 0, sizeof(k));
+	if (klen > 64) {
+		struct hctx t;
+		h_init(&t, alg);
+		h_update(&t, key, (size_t)klen);
+		h_final(k, &t);
+	} else {
+		memcpy(k, key, (size_t)klen);
+	}
+	for (int i = 0; i < 64; i++)
+		k[i] ^= padval;
+	h_init(c, alg);
+	h_update(c, k, 64);
+}
+
+void oref_hmac(int alg, const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t *out)
+{
+	struct hctx i, o;
+	uint8_t inner[32];
+
+	h_hmac_pad(key, klen, &i, alg, 0x36);
+	h_hmac_pad(key, klen, &o, alg, 0x5c);
+	h_update(&i, msg, len);
+	h_final(inner, &i);
+	h_update(&o, inner, (size_t)hash_len(alg));
+	h_final(out, &o);
+}
+
+/* AES-ICM over data from an explicit 16-byte initial counter block
+ * (aes_icm_reinit + aes_icm_crypt/_last, xform_aes_icm.c:113-181) */
+void oref_aes_ctr(const uint8_t *key, int klen, const uint8_t ctr[16], uint8_t *data, int len)
+{
+	struct icm_ctx c;
+	int resid;
+
+	init_tables();
+	c.nr = oref_aes_setkey_enc(c.ek, key, klen * 8);
+	memcpy(c.block, ctr, 16);
+	for (resid = len; resid >= 16; resid -= 16, data += 16)
+		icm_crypt(&c, data, data);
+	if (resid > 0)
+		icm_crypt_last(&c, data, data, resid);
+}
+
+/* ------------------------------------------------------------------------ */
 /* Sessions (cryptosoft.c:976-1128, 1309-1409)                               */
 
 struct oref_sa {
 	int mode, flags, mlen, klen;
+	int calg, aalg;         /* ETA: AES_CBC or AES_ICM; SHA1_HMAC or SHA2_256_HMAC */
 	uint8_t salt[4];
 	/* GCM: sw_ictx (AES-GMAC ctx) + sw_kschedule (ICM ctx) */
 	struct gmac_ctx gictx;
@@ -604,11 +771,18 @@ struct oref_sa {
 	/* ETA: rijndael ctx + HMAC ipad/opad contexts */
 	uint32_t ek[60], dk[60];
 	int nr;
-	struct sha1_ctx ictx, octx;
+	struct hctx ictx, octx;
 };
 
 oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
     const uint8_t salt[4], const uint8_t *akey, int aklen, int mlen)
+{
+	return oref_sa_new2(mode, flags, mode == OREF_CSP_MODE_AEAD ? OREF_CRYPTO_AES_NIST_GCM_16 :
+	    OREF_CRYPTO_AES_CBC, ckey, cklen, salt, OREF_CRYPTO_SHA1_HMAC, akey, aklen, mlen);
+}
+
+oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int cklen,
+    const uint8_t salt[4], int aalg, const uint8_t *akey, int aklen, int mlen)
 {
 	oref_sa *sa;
 
@@ -628,11 +802,20 @@ oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
 		if (salt)
 			memcpy(sa->salt, salt, 4);
 	} else if (mode == OREF_CSP_MODE_ETA) {         /* swcr_setup_cipher/auth */
-		sa->mlen = (mlen == 0) ? 20 : mlen;
+		if ((calg != OREF_CRYPTO_AES_CBC && calg != OREF_CRYPTO_AES_ICM) ||
+		    (aalg != OREF_CRYPTO_SHA1_HMAC && aalg != OREF_CRYPTO_SHA2_256_HMAC)) {
+			free(sa);
+			return NULL;
+		}
+		sa->calg = calg;
+		sa->aalg = aalg;
+		sa->mlen = (mlen == 0) ? hash_len(aalg) : mlen;   /* :1013-1018 */
 		sa->nr = oref_aes_setkey_enc(sa->ek, ckey, cklen * 8);
 		oref_aes_setkey_dec(sa->dk, ckey, cklen * 8);
-		hmac_pad(akey, aklen, &sa->ictx, 0x36);
-		hmac_pad(akey, aklen, &sa->octx, 0x5c);
+		if (salt)
+			memcpy(sa->salt, salt, 4);      /* AES-ICM nonce (RFC 3686) */
+		h_hmac_pad(akey, aklen, &sa->ictx, aalg, 0x36);
+		h_hmac_pad(akey, aklen, &sa->octx, aalg, 0x5c);
 	} else {
 		free(sa);
 		return NULL;
@@ -731,12 +914,25 @@ static int swcr_gcm_c(const oref_sa *sa, struct req *r)
 	return 0;
 }
 
-/* swcr_encdec for AES-CBC on a contiguous buffer (cryptosoft.c:101-284) */
+/* swcr_encdec for AES-CBC / AES-ICM on a contiguous buffer (cryptosoft.c:101-284) */
 static int swcr_encdec_cbc(const oref_sa *sa, struct req *r)
 {
 	uint8_t iv[16], niv[16];
 	uint8_t *p = r->buf + r->payload_start;
 
+	if (sa->calg == OREF_CRYPTO_AES_ICM) {          /* stream cipher: any length */
+		struct icm_ctx c;
+		int resid;
+
+		memcpy(c.ek, sa->ek, sizeof(c.ek));
+		c.nr = sa->nr;
+		memcpy(c.block, r->iv, 16);             /* aes_icm_reinit, IV_SEPARATE */
+		for (resid = r->payload_len; resid >= 16; resid -= 16, p += 16)
+			icm_crypt(&c, p, p);
+		if (resid > 0)
+			icm_crypt_last(&c, p, p, resid);
+		return 0;
+	}
 	if (r->payload_len % 16)
 		return EINVAL;
 	memcpy(iv, r->buf + r->iv_start, 16);           /* crypto_read_iv */
@@ -757,21 +953,21 @@ static int swcr_encdec_cbc(const oref_sa *sa, struct req *r)
 	return 0;
 }
 
-/* swcr_authcompute for HMAC-SHA1 (cryptosoft.c:317-382) */
+/* swcr_authcompute for HMAC-SHA1 / HMAC-SHA2-256 (cryptosoft.c:317-382) */
 static int swcr_authcompute_c(const oref_sa *sa, struct req *r)
 {
-	struct sha1_ctx ctx;
-	uint8_t a[20];
+	struct hctx ctx;
+	uint8_t a[32];
 
 	memcpy(&ctx, &sa->ictx, sizeof(ctx));
-	sha1_update(&ctx, r->buf + r->aad_start, (size_t)r->aad_len);
-	sha1_update(&ctx, r->buf + r->payload_start, (size_t)r->payload_len);
+	h_update(&ctx, r->buf + r->aad_start, (size_t)r->aad_len);
+	h_update(&ctx, r->buf + r->payload_start, (size_t)r->payload_len);
 	if (sa->flags & OREF_CSP_F_ESN)
-		sha1_update(&ctx, r->esn, 4);
-	sha1_final(a, &ctx);
+		h_update(&ctx, r->esn, 4);
+	h_final(a, &ctx);
 	memcpy(&ctx, &sa->octx, sizeof(ctx));
-	sha1_update(&ctx, a, 20);
-	sha1_final(a, &ctx);
+	h_update(&ctx, a, (size_t)hash_len(sa->aalg));
+	h_final(a, &ctx);
 	if (!r->encrypt) {
 		uint8_t diff = 0;
 		for (int i = 0; i < sa->mlen; i++)
@@ -801,14 +997,15 @@ static int esp_process(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi
 	struct req r;
 	uint8_t aadbuf[12];
 	int gcm = (sa->mode == OREF_CSP_MODE_AEAD);
-	int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen;
+	int ctr = !gcm && sa->calg == OREF_CRYPTO_AES_ICM;
+	int ivlen = (gcm || ctr) ? 8 : 16, hlen = 8 + ivlen;   /* RFC 4106 / 3686: 8-byte IV */
 	/* ICV bytes = the session's sw_mlen (cryptosoft.c:1112-1117): 16 for GCM
 	 * and 12 for HMAC-SHA1-96 as ESP sets them up (xform_ah_authsize), 8/12
 	 * for a truncated GCM session, 20 for an untruncated HMAC-SHA1 one */
 	int alen = sa->mlen;
 	int plen = len - hlen - alen;
 
-	if ((len & 3) || plen <= 0 || (!gcm && (plen & 15)))   /* :279-324 */
+	if ((len & 3) || plen <= 0 || (!gcm && !ctr && (plen & 15)))   /* :279-324 */
 		return EINVAL;
 	memset(&r, 0, sizeof(r));
 	r.buf = esp;
@@ -833,6 +1030,11 @@ static int esp_process(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi
 	r.aad_start = 0;
 	r.aad_len = hlen;                               /* :369 */
 	r.iv_start = hlen - ivlen;                      /* :460-461 */
+	if (ctr) {                                      /* :453-458: salt | IV | be32(1) */
+		memcpy(r.iv, sa->salt, 4);
+		memcpy(r.iv + 4, esp + 8, 8);
+		st_be32(r.iv + 12, 1);
+	}
 	return swcr_eta_c(sa, &r);
 }
 

@@ -38,6 +38,8 @@ extern "C" {
 /* algorithms (cryptodev.h:150-169) */
 #define OREF_CRYPTO_SHA1_HMAC      7
 #define OREF_CRYPTO_AES_CBC        11
+#define OREF_CRYPTO_SHA2_256_HMAC  18
+#define OREF_CRYPTO_AES_ICM        23          /* AES-CTR */
 #define OREF_CRYPTO_AES_NIST_GCM_16 25
 
 typedef struct oref_sa oref_sa;
@@ -51,6 +53,11 @@ void oref_aes_decrypt(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t 
 void oref_gf128_mul(const uint8_t h[16], const uint8_t x[16], uint8_t out[16]);
 void oref_sha1(const uint8_t *msg, size_t len, uint8_t out[20]);
 void oref_hmac_sha1(const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t out[20]);
+void oref_sha256(const uint8_t *msg, size_t len, uint8_t out[32]);
+/* HMAC with alg = OREF_CRYPTO_SHA1_HMAC (20-byte out) or _SHA2_256_HMAC (32) */
+void oref_hmac(int alg, const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t *out);
+/* AES-ICM (counter mode, full 128-bit big-endian increment) from ctr[16] */
+void oref_aes_ctr(const uint8_t *key, int klen, const uint8_t ctr[16], uint8_t *data, int len);
 
 /* Generic AES-GCM AEAD (12-byte IV) as swcr_gcm computes it; in place.
  * encrypt: writes tag[16].  decrypt: verifies tag[0..mlen) and returns
@@ -71,6 +78,11 @@ int oref_eta(const uint8_t *ckey, int cklen, const uint8_t *akey, int aklen,
  * ETA: AES-CBC cipher key + HMAC-SHA1 key, mlen 12 (AH_HMAC_HASHLEN). */
 oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
                      const uint8_t salt[4], const uint8_t *akey, int aklen, int mlen);
+/* ETA with a chosen cipher (OREF_CRYPTO_AES_CBC, or _AES_ICM: RFC 3686 ESP
+ * AES-CTR, salt = the 4-byte nonce esp_init strips from the key) and HMAC
+ * (OREF_CRYPTO_SHA1_HMAC or _SHA2_256_HMAC; mlen 0 = the full hash). */
+oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int cklen,
+                      const uint8_t salt[4], int aalg, const uint8_t *akey, int aklen, int mlen);
 void oref_sa_free(oref_sa *sa);
 
 /* ESP record = [SPI 4][SN 4][IV ivlen][payload][ICV alen], i.e. the buffer

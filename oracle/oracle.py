@@ -14,6 +14,10 @@ REF_PATH = os.path.join(HERE, "_ref", "libref.so")
 
 CSP_MODE_AEAD = 4
 CSP_MODE_ETA = 5
+CRYPTO_SHA1_HMAC = 7
+CRYPTO_AES_CBC = 11
+CRYPTO_SHA2_256_HMAC = 18
+CRYPTO_AES_ICM = 23
 CSP_F_SEPARATE_AAD = 0x2
 CSP_F_ESN = 0x4
 EBADMSG = 74
@@ -32,7 +36,13 @@ def lib():
         L.oref_sa_new.restype = C.c_void_p
         L.oref_sa_new.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_char_p,
                                   C.c_char_p, C.c_int, C.c_int]
+        L.oref_sa_new2.restype = C.c_void_p
+        L.oref_sa_new2.argtypes = [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_char_p,
+                                   C.c_int, C.c_char_p, C.c_int, C.c_int]
         L.oref_sa_free.argtypes = [C.c_void_p]
+        L.oref_sha256.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p]
+        L.oref_hmac.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_size_t, C.c_void_p]
+        L.oref_aes_ctr.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_void_p, C.c_int]
         L.oref_esp_decrypt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
         L.oref_esp_encrypt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
         L.oref_gcm.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int,
@@ -59,10 +69,13 @@ def lib():
 class SA:
     """A cryptosoft-style session (swcr_newsession)."""
 
-    def __init__(self, mode, ckey, salt=b"\0\0\0\0", akey=b"", mlen=0, flags=0):
+    def __init__(self, mode, ckey, salt=b"\0\0\0\0", akey=b"", mlen=0, flags=0,
+                 calg=CRYPTO_AES_CBC, aalg=CRYPTO_SHA1_HMAC):
+        """ETA: calg CRYPTO_AES_CBC or CRYPTO_AES_ICM (ESP AES-CTR, salt = the
+        RFC 3686 nonce), aalg CRYPTO_SHA1_HMAC or CRYPTO_SHA2_256_HMAC."""
         self.mode = mode
-        self.h = lib().oref_sa_new(mode, flags, bytes(ckey), len(ckey), bytes(salt),
-                                   bytes(akey), len(akey), mlen)
+        self.h = lib().oref_sa_new2(mode, flags, calg, bytes(ckey), len(ckey), bytes(salt),
+                                    aalg, bytes(akey), len(akey), mlen)
         if not self.h:
             raise ValueError("oref_sa_new failed")
 
@@ -98,6 +111,25 @@ def eta(ckey, akey, iv, aad, data, digest=b"\0" * 20, mlen=20, encrypt=True):
     e = lib().oref_eta(bytes(ckey), len(ckey), bytes(akey), len(akey), bytes(iv), bytes(aad),
                        len(aad), buf, len(data), d, mlen, 1 if encrypt else 0)
     return e, buf.raw[:len(data)], d.raw
+
+
+def sha256(msg):
+    out = C.create_string_buffer(32)
+    lib().oref_sha256(bytes(msg), len(msg), out)
+    return out.raw
+
+
+def hmac(alg, key, msg):
+    out = C.create_string_buffer(32)
+    lib().oref_hmac(alg, bytes(key), len(key), bytes(msg), len(msg), out)
+    return out.raw[:32 if alg == CRYPTO_SHA2_256_HMAC else 20]
+
+
+def aes_ctr(key, ctr16, data):
+    """AES-ICM (full 128-bit counter increment) starting at ctr16."""
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    lib().oref_aes_ctr(bytes(key), len(key), bytes(ctr16), buf, len(data))
+    return buf.raw[:len(data)]
 
 
 def aes_encrypt_block(key, block):

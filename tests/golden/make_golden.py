@@ -12,6 +12,10 @@ plain-data JSON fixtures next to this script:
                      test_cryptodev_aead_test_vectors.h:88-434,1037-1687,1740-1793
   cbc_hmac_sha1.json AES-CBC + HMAC-SHA1 chained KATs (encrypt-then-MAC over CT)
                      test_cryptodev_aes_test_vectors.h:1492,2187,2309
+  eta_esp_packets.json  complete ESP tunnel packets, AES-CBC + HMAC-SHA2-256-128
+                     test_cryptodev_security_ipsec_test_vectors.h:744,1721
+  ctr_hmac_sha1.json AES-CTR (full 128-bit counter) + HMAC-SHA1 chained KATs
+                     test_cryptodev_aes_test_vectors.h:1221,1311,1358,1447
 
 The JSON holds only inputs and expected outputs (hex strings); no reference
 source text is stored.  Usage:  python tests/golden/make_golden.py
@@ -240,12 +244,68 @@ def cbc_hmac_sha1():
     return out
 
 
+def eta_esp_packets():
+    """ESP packets of CBC + HMAC-SHA2-256 SAs (ICV = 16 bytes, RFC 4868)."""
+    path = os.path.join(TESTDIR, "test_cryptodev_security_ipsec_test_vectors.h")
+    structs = parse_structs(path, r"struct\s+ipsec_test_data")
+    out = []
+    for name in ["pkt_aes_128_cbc_hmac_sha256", "pkt_aes_128_cbc_hmac_sha256_v6"]:
+        s = structs[name]
+        ch = s["xform"]["chain"]
+        cipher, auth = ch["cipher"]["cipher"], ch["auth"]["auth"]
+        assert cipher["algo"] == "RTE_CRYPTO_CIPHER_AES_CBC" and auth["algo"] == "RTE_CRYPTO_AUTH_SHA256_HMAC"
+        outer = s["output_text"]["data"][: s["output_text"]["len"]]
+        inner = s["input_text"]["data"][: s["input_text"]["len"]]
+        ver = outer[0] >> 4
+        iphl = (outer[0] & 0xF) * 4 if ver == 4 else 40
+        out.append({
+            "name": name,
+            "source": "dpdk/app/test/test_cryptodev_security_ipsec_test_vectors.h",
+            "mode": "cbc-hmac-sha256",
+            "cipher_key": hexs(data_of(s["key"], {}, cipher["key"]["length"])),
+            "auth_key": hexs(data_of(s["auth_key"], {}, auth["key"]["length"])),
+            "digest_len": auth["digest_length"],
+            "spi": s["ipsec_xform"]["spi"],
+            "outer_hdr_len": iphl,
+            "esp_record": hexs(outer[iphl:]),
+            "inner_packet": hexs(inner),
+        })
+    return out
+
+
+def ctr_hmac_sha1():
+    """AES-CTR chained with HMAC-SHA1 (digest over the ciphertext); the IV is
+    the whole initial counter block (16 bytes) or a 12-byte nonce whose
+    32-bit counter starts at 1 (RFC 3686 layout, test_cryptodev_blockcipher.c)."""
+    path = os.path.join(TESTDIR, "test_cryptodev_aes_test_vectors.h")
+    arrays = parse_arrays(path)
+    structs = parse_structs(path, r"static\s+const\s+struct\s+blockcipher_test_data")
+    out = []
+    for name in ["aes_test_data_1", "aes_test_data_3", "aes_test_data_1_IV_12_bytes",
+                 "aes_test_data_3_IV_12_bytes"]:
+        s = structs[name]
+        assert s["crypto_algo"] == "RTE_CRYPTO_CIPHER_AES_CTR" and s["auth_algo"] == "RTE_CRYPTO_AUTH_SHA1_HMAC"
+        out.append({
+            "name": name,
+            "source": "dpdk/app/test/test_cryptodev_aes_test_vectors.h",
+            "cipher_key": hexs(data_of(s["cipher_key"], arrays)),
+            "iv": hexs(data_of(s["iv"], arrays)),
+            "plaintext": hexs(data_of(s["plaintext"], arrays)),
+            "ciphertext": hexs(data_of(s["ciphertext"], arrays)),
+            "auth_key": hexs(data_of(s["auth_key"], arrays)),
+            "digest": hexs(data_of(s["digest"], arrays)),
+            "truncated_len": s["digest"].get("truncated_len", 20),
+        })
+    return out
+
+
 def main():
     if not os.path.isdir(TESTDIR):
         print("reference tree not found at %s" % TESTDIR, file=sys.stderr)
         return 1
     for fname, fn in (("esp_packets.json", esp_packets), ("gcm_aead.json", gcm_aead),
-                      ("cbc_hmac_sha1.json", cbc_hmac_sha1)):
+                      ("cbc_hmac_sha1.json", cbc_hmac_sha1), ("eta_esp_packets.json", eta_esp_packets),
+                      ("ctr_hmac_sha1.json", ctr_hmac_sha1)):
         vecs = fn()
         with open(os.path.join(OUT, fname), "w") as f:
             json.dump(vecs, f, indent=1)

@@ -197,3 +197,81 @@ def test_esp_truncated_icv_is_tag_prefix(mlen):
         bad[-1] ^= 0x04
         e, out = trunc.esp_decrypt(bytes(bad))
         assert e == O.EBADMSG and out == bytes(bad)
+
+
+# ---------------------------------------------------------------------------
+# f4: AES-CTR (AES-ICM, RFC 3686 in ESP) and HMAC-SHA2-256 ETA sessions
+
+@pytest.mark.parametrize("v", golden("ctr_hmac_sha1.json"), ids=lambda v: v["name"])
+def test_ctr_hmac_sha1_kat(v):
+    """DPDK AES-CTR + HMAC-SHA1 KATs: the oracle's AES-ICM (full 128-bit
+    counter increment, xform_aes_icm.c:160-166) and HMAC-SHA1 over the CT.
+    A 12-byte IV is an RFC 3686-style nonce whose 32-bit counter starts at 1."""
+    key, iv = bytes.fromhex(v["cipher_key"]), bytes.fromhex(v["iv"])
+    ctr = iv if len(iv) == 16 else iv + (1).to_bytes(4, "big")
+    ct = O.aes_ctr(key, ctr, bytes.fromhex(v["plaintext"]))
+    assert ct.hex() == v["ciphertext"]
+    assert O.aes_ctr(key, ctr, ct).hex() == v["plaintext"]
+    n = v["truncated_len"]
+    assert O.hmac(O.CRYPTO_SHA1_HMAC, bytes.fromhex(v["auth_key"]), ct)[:n].hex() == v["digest"][:2 * n]
+
+
+def test_sha256_hmac_against_hashlib():
+    rng = np.random.default_rng(8)
+    for n in (0, 1, 55, 56, 63, 64, 65, 119, 1000, 1464):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert O.sha256(m) == hashlib.sha256(m).digest()
+        k = rng.integers(0, 256, (n % 90) + 1, dtype=np.uint8).tobytes()
+        assert O.hmac(O.CRYPTO_SHA2_256_HMAC, k, m) == hmac.new(k, m, hashlib.sha256).digest()
+
+
+@pytest.mark.parametrize("v", golden("eta_esp_packets.json"), ids=lambda v: v["name"])
+def test_eta_sha256_esp_packet_kat(v):
+    """DPDK ESP tunnel packets under AES-CBC + HMAC-SHA2-256-128 (ICV 16 =
+    hashsize/2, xform_ah.c:125-128): decrypt gives the inner packet, encrypt
+    gives back the packet, a flipped ICV bit is EBADMSG with the record
+    untouched."""
+    sa = O.SA(O.CSP_MODE_ETA, bytes.fromhex(v["cipher_key"]), akey=bytes.fromhex(v["auth_key"]),
+              mlen=v["digest_len"], aalg=O.CRYPTO_SHA2_256_HMAC)
+    rec = bytes.fromhex(v["esp_record"])
+    e, out = sa.esp_decrypt(rec)
+    assert e == 0
+    inner = bytes.fromhex(v["inner_packet"])
+    pt = out[24:len(out) - v["digest_len"]]
+    assert pt[:len(inner)] == inner
+    padlen = pt[-2]
+    assert len(pt) == len(inner) + padlen + 2
+    e2, again = sa.esp_encrypt(out)
+    assert e2 == 0 and again == rec
+    bad = bytearray(rec)
+    bad[-1] ^= 0x01
+    e3, out3 = sa.esp_decrypt(bytes(bad))
+    assert e3 == O.EBADMSG and out3 == bytes(bad)
+
+
+@pytest.mark.parametrize("aalg,mlen", [(O.CRYPTO_SHA1_HMAC, 12), (O.CRYPTO_SHA2_256_HMAC, 16)])
+@pytest.mark.parametrize("klen", [16, 32])
+def test_esp_ctr_record_layout(aalg, mlen, klen):
+    """ESP AES-CTR (RFC 3686; esp_input xform_esp.c:453-458): counter block =
+    nonce(4) || explicit IV(8) || be32(1), AAD = SPI || SN || IV (hlen 16),
+    any 4-byte-multiple payload; the ICV is the first mlen bytes of the HMAC
+    over AAD || CT.  Checked against the primitive KAT functions."""
+    rng = np.random.default_rng(90 + klen + mlen)
+    key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+    nonce = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+    akey = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    sa = O.SA(O.CSP_MODE_ETA, key, nonce, akey=akey, mlen=mlen, calg=O.CRYPTO_AES_ICM, aalg=aalg)
+    for plen in (4, 16, 100, 1448, 4096 + 12):
+        hdr = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        pt = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        e, rec = sa.esp_encrypt(hdr + pt + bytes(mlen))
+        assert e == 0
+        ct = O.aes_ctr(key, nonce + hdr[8:16] + (1).to_bytes(4, "big"), pt)
+        assert rec[16:16 + plen] == ct
+        assert rec[16 + plen:] == O.hmac(aalg, akey, hdr + ct)[:mlen]
+        e, dec = sa.esp_decrypt(rec)
+        assert e == 0 and dec[16:16 + plen] == pt
+        bad = bytearray(rec)
+        bad[-2] ^= 0x40
+        e, out = sa.esp_decrypt(bytes(bad))
+        assert e == O.EBADMSG and out == bytes(bad)
