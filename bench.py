@@ -279,7 +279,7 @@ def launched_kernel(cfg, inplace):
     verify-first; eta_kernel<DECRYPT> for CBC + HMAC-SHA1."""
     if cfg["alg"] == "gcm":
         return "gcm_kernel<%d, 1024>" % (2 if inplace else 0)
-    return "eta_kernel<%d, 768>" % (2 if inplace else 0)
+    return "eta_kernel<2, 768, -1>" if inplace else "eta_kernel<0, 768, 0>"   # CBC sessions
 
 
 def profile_traffic(config, inplace, kernel, kern_ms):

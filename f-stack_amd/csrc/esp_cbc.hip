@@ -1,31 +1,39 @@
-// esp_cbc.hip — ESP AES-CBC + HMAC-SHA1-96 (CSP_MODE_ETA) kernels for gfx950.
+// esp_cbc.hip — ESP encrypt-then-MAC (CSP_MODE_ETA) kernels for gfx950:
+// AES-CBC or AES-CTR (RFC 3686) with HMAC-SHA1 or HMAC-SHA2-256.
 //
 // Replaces swcr_eta (freebsd/opencrypto/cryptosoft.c:874-888) =
-//   decrypt: swcr_authcompute (verify, :317-382) then swcr_encdec (CBC, :101-284)
+//   decrypt: swcr_authcompute (verify, :317-382) then swcr_encdec (:101-284)
 //   encrypt: swcr_encdec then swcr_authcompute (compute, ICV written)
 // for the request esp_input / esp_output build (xform_esp.c:296-461):
-//   AAD = ESP header + IV (hlen = 8 + 16 bytes), payload = CBC ciphertext,
-//   HMAC-SHA1 over AAD || payload (|| ESN high 32 bits, CSP_F_ESN), ICV = the
-//   first mlen (12) bytes, IV = the 16 bytes before the payload.
+//   CBC: record = SPI|SN|IV16|CT|ICV, hlen 24, IV = the 16 bytes before the CT,
+//        CT a multiple of 16 (rijndael blocksize);
+//   CTR: record = SPI|SN|IV8|CT|ICV, hlen 16, counter block of CT block i =
+//        nonce(4) || IV8 || be32(i+1) (xform_esp.c:453-458, RFC 3686; the nonce
+//        is the SA key's last 4 bytes, carried in the descriptor's salt), any
+//        4-byte-multiple CT (blocksize 1, esp_output pads to 4);
+//   HMAC over SPI|SN|IV|CT (|| ESN high word, CSP_F_ESN); ICV = its first mlen
+//   bytes (12 for SHA1-96, 16 for SHA2-256-128: xform_ah_authsize).
 //
 // Mapping: a wave owns 64 records (lane = record for everything serial).
-//  * HMAC-SHA1 is a serial chain per record, so lane = record: each lane runs
-//    its record's SHA-1 compressions from the precomputed ipad/opad chaining
-//    states (hmac_init_pad, crypto.c:413-441), 80 rounds fully unrolled in
-//    registers, no tables.
+//  * HMAC is a serial chain per record, so lane = record: each lane runs its
+//    record's SHA-1 / SHA-256 compressions from the precomputed ipad/opad
+//    chaining states (hmac_init_pad, crypto.c:413-441), rounds fully
+//    unrolled in registers, no tables.
 //  * Out-of-place decrypt (MODE 0, the benchmarked path) is ONE pass per
 //    record (eta_decrypt_fused): every 64-byte HMAC chunk the lane loads also
-//    completes up to four CBC blocks, which it decrypts with four AES states
-//    in flight (aes_dec4) and stores, so the record is read once.
+//    completes up to four cipher blocks, which it decrypts with four AES
+//    states in flight (aes_dec4 for CBC, aes_enc4 of the counters for CTR)
+//    and stores, so the record is read once.
 //  * In-place verify-first decrypt (MODE 2) must authenticate before it may
-//    overwrite: HMAC pass first, then the CBC pass is block-parallel -- the
-//    wave walks its records as one flat block list, 64 consecutive blocks per
-//    pass (1 KiB contiguous per instruction), last pass first, so in-place
+//    overwrite: HMAC pass first, then a block-parallel pass -- the wave walks
+//    its records as one flat block list, 64 consecutive blocks per pass
+//    (1 KiB contiguous per instruction), last pass first, so in-place CBC
 //    decryption never reads a block another lane already overwrote.
-//  * AES decryption uses Td0/Td1 tables replicated 32x in LDS (conflict-free
-//    ds_read_b32, one v_perm_b32 per address, as in esp_gcm.hip) and a
-//    replicated inverse S-box for the last round.
-//  * CBC encryption is serial per record (lane = record), Te0/Te1 in LDS.
+//  * AES uses T-table pairs replicated 32x in LDS (conflict-free ds_read_b32,
+//    one v_perm_b32 per address, as in esp_gcm.hip): Td0/Td1 + a replicated
+//    inverse S-box for CBC decryption, Te0/Te1 for CBC encryption and CTR.
+//  * CBC encryption is serial per record (lane = record); CTR encryption runs
+//    the same lane = record loop with independent blocks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,15 +44,17 @@ namespace espgpu {
 
 namespace {
 
+// LDS: decrypt modes hold Td pair, inverse S-box and Te pair (CBC and CTR
+// sessions can share a launch); encrypt holds the Te pair only.
 constexpr uint32_t LDS_T = 0;          // Td0/Td1 (decrypt) or Te0/Te1 (encrypt), 64 KiB
 constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32 KiB
-constexpr uint32_t LDS_BYTES = 65536 + 32768;
+constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
+constexpr uint32_t lds_bytes(int mode) { return mode == 1 ? 65536u : 163840u; }
+
+constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
+constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
 
 typedef const __attribute__((address_space(4))) uint32_t *kptr;
-
-struct __attribute__((aligned(4))) U4 {
-  uint32_t x, y, z, w;
-};
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -54,19 +64,44 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 }
 __device__ __forceinline__ uint32_t ror16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return perm(x, x, 0x00010203u); }
+// single 16- / 8-byte vector accesses at 4-byte alignment (see esp_gcm.hip)
+typedef uint32_t V4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t V2a __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-  U4 v = *reinterpret_cast<const U4 *>(p);
+  const V4a v = *reinterpret_cast<const V4a *>(p);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
-  *reinterpret_cast<U4 *>(p) = U4{v.x, v.y, v.z, v.w};
+  V4a u = {v.x, v.y, v.z, v.w};
+  *reinterpret_cast<V4a *>(p) = u;
+}
+// first `rem` bytes (4, 8, 12 or >= 16) of v; no store shared with the full
+// path, so full blocks stay single 16-byte stores
+__device__ __forceinline__ void st_partial(uint8_t *p, uint4 v, int rem) {
+  if (rem >= 16) {
+    st16(p, v);
+    return;
+  }
+  if (rem > 4) {
+    V2a u = {v.x, v.y};
+    *reinterpret_cast<V2a *>(p) = u;
+  } else {
+    *reinterpret_cast<uint32_t *>(p) = v.x;
+  }
+  if (rem > 8) *reinterpret_cast<uint32_t *>(p + 8) = v.z;
 }
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 __device__ __forceinline__ uint4 bswap4(uint4 v) {
   return make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+}
+// the dword of a block holding the last 3 plaintext bytes, rem = bytes of the
+// block that are payload (4, 8, 12 or 16)
+__device__ __forceinline__ uint32_t last_word(uint4 v, int rem) {
+  return rem >= 16 ? v.w : (rem > 8 ? v.z : (rem > 4 ? v.y : v.x));
 }
 
 // T-table addressing, see esp_gcm.hip: entry x at x*256, T0 in lane slots
@@ -207,6 +242,54 @@ __device__ __forceinline__ uint4 aes_enc(uint4 in, KP ek, int nr, const uint8_t 
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// Four independent blocks through the encryption rounds (CTR keystream of
+// one 64-byte chunk): Te0/Te1 at `lds`, round keys `ek` (enc schedule).
+template <typename KP>
+__device__ __forceinline__ void aes_enc4(uint4 (&v)[4], KP ek, int nr, const uint8_t *lds, uint32_t slot) {
+  uint32_t s[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s[q][0] = bswap32(v[q].x) ^ ek[0];
+    s[q][1] = bswap32(v[q].y) ^ ek[1];
+    s[q][2] = bswap32(v[q].z) ^ ek[2];
+    s[q][3] = bswap32(v[q].w) ^ ek[3];
+  }
+#pragma unroll 1
+  for (int r = 1; r < nr; ++r) {
+    const uint32_t k0 = ror16(ek[4 * r]), k1 = ror16(ek[4 * r + 1]);
+    const uint32_t k2 = ror16(ek[4 * r + 2]), k3 = ror16(ek[4 * r + 3]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t s0 = s[q][0], s1 = s[q][1], s2 = s[q][2], s3 = s[q][3];
+      const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s1, slot, 2));
+      const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s3, slot, 0));
+      const uint32_t a1 = t0(lds, tpa(s1, slot, 3)), b1 = t1(lds, tpa(s2, slot, 2));
+      const uint32_t c1 = t0(lds, tpa(s3, slot, 1)), d1 = t1(lds, tpa(s0, slot, 0));
+      const uint32_t a2 = t0(lds, tpa(s2, slot, 3)), b2 = t1(lds, tpa(s3, slot, 2));
+      const uint32_t c2 = t0(lds, tpa(s0, slot, 1)), d2 = t1(lds, tpa(s1, slot, 0));
+      const uint32_t a3 = t0(lds, tpa(s3, slot, 3)), b3 = t1(lds, tpa(s0, slot, 2));
+      const uint32_t c3 = t0(lds, tpa(s1, slot, 1)), d3 = t1(lds, tpa(s2, slot, 0));
+      s[q][0] = xor3(a0, b0, ror16(xor3(c0, d0, k0)));
+      s[q][1] = xor3(a1, b1, ror16(xor3(c1, d1, k1)));
+      s[q][2] = xor3(a2, b2, ror16(xor3(c2, d2, k2)));
+      s[q][3] = xor3(a3, b3, ror16(xor3(c3, d3, k3)));
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t a = t0(lds, tpa(s[q][c], slot, 3));
+      const uint32_t b = t0(lds, tpa(s[q][(c + 1) & 3], slot, 2));
+      const uint32_t cc = t0(lds, tpa(s[q][(c + 2) & 3], slot, 1));
+      const uint32_t d = t0(lds, tpa(s[q][(c + 3) & 3], slot, 0));
+      o[c] = xor3(perm(b, a, 0x0c0c0501u), perm(d, cc, 0x05010c0cu), bswap32(ek[4 * nr + c]));
+    }
+    v[q] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // ---- SHA-1 compression (sha1_step, freebsd/crypto/sha1.c:94-176) ----------
 __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
@@ -243,175 +326,272 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
 }
 
-// HMAC-SHA1 of msg = rec[0, L0) || (esn ? be32(esn_hi) : "") from the SA's
+// ---- SHA-256 compression (SHA256_Transform, freebsd/crypto/sha2/sha256c.c:135) ----
+__constant__ uint32_t kK256[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u,
+};
+
+__device__ __forceinline__ void sha256_compress(uint32_t h[8], uint32_t w[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
+      const uint32_t s0 = xor3(rotr(x, 7), rotr(x, 18), x >> 3);
+      const uint32_t s1 = xor3(rotr(y, 17), rotr(y, 19), y >> 10);
+      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);     // (e & f) | (~e & g)
+    const uint32_t t1 = hh + S1 + ch + kK256[t] + wt;
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);     // majority
+    hh = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// The two HMAC hashes behind one interface: W chaining words.
+template <int HS> struct Hash;
+template <> struct Hash<HS_SHA1> {
+  static constexpr int W = 5;
+  static __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) { sha1_compress(h, w); }
+};
+template <> struct Hash<HS_SHA256> {
+  static constexpr int W = 8;
+  static __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) { sha256_compress(h, w); }
+};
+
+// message word k of the padded block b of the inner HMAC message
+// rec[0, L0) || (esn ? be32(esn_hi) : "") once past the full blocks
+__device__ __forceinline__ uint32_t tail_word(const uint8_t *rec, uint32_t b, int k, uint32_t L0, uint32_t L,
+                                              bool esn, uint32_t esn_hi, uint32_t total, uint64_t bits) {
+  const uint32_t o = 64 * b + 4 * k;
+  uint32_t v;
+  if (o + 4 <= L0) v = bswap32(*reinterpret_cast<const uint32_t *>(rec + o));
+  else if (esn && o == L0) v = esn_hi;
+  else if (o == L) v = 0x80000000u;
+  else v = 0;
+  if (b == total - 1 && k == 14) v = (uint32_t)(bits >> 32);
+  if (b == total - 1 && k == 15) v = (uint32_t)bits;
+  return v;
+}
+
+// the outer block: inner digest || 0x80 || 0... || bit length of (64 + digest)
+template <int HS>
+__device__ __forceinline__ void outer_block(const uint32_t h[8], uint32_t w[16]) {
+  constexpr int W = Hash<HS>::W;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = k < W ? h[k] : (k == W ? 0x80000000u : 0u);
+  w[15] = (64 + 4 * W) * 8;
+}
+
+// HMAC of msg = rec[0, L0) || (esn ? be32(esn_hi) : "") from the SA's
 // ipad/opad chaining states (already past the 64-byte key block).
-__device__ void hmac_sha1(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi,
-                          kptr ipad, kptr opad, uint32_t out[5]) {
+template <int HS>
+__device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi, kptr ipad, kptr opad,
+                       uint32_t out[8]) {
+  constexpr int W = Hash<HS>::W;
   const uint32_t L = L0 + (esn ? 4u : 0u);              // multiple of 4 for ESP records
   const uint32_t nfull = L0 / 64;                       // blocks entirely from memory
   const uint32_t total = (L + 9 + 63) / 64;             // inner blocks incl. padding
   const uint64_t bits = (uint64_t)(64 + L) * 8;         // the ipad block counts
-  uint32_t h[5] = {ipad[0], ipad[1], ipad[2], ipad[3], ipad[4]};
+  uint32_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = k < W ? ipad[k] : 0u;
   uint32_t w[16];
   // One compression site for every block (inner data, inner padding, outer)
-  // keeps a single inlined copy of the 80 rounds.
+  // keeps a single inlined copy of the rounds.
   for (uint32_t b = 0; b <= total; ++b) {
     if (b < nfull) {
       const uint8_t *p = rec + 64 * b;
-      const uint4 q0 = bswap4(ld16(p)), q1 = bswap4(ld16(p + 16)), q2 = bswap4(ld16(p + 32)),
-                  q3 = bswap4(ld16(p + 48));
-      w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w;
-      w[4] = q1.x; w[5] = q1.y; w[6] = q1.z; w[7] = q1.w;
-      w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
-      w[12] = q3.x; w[13] = q3.y; w[14] = q3.z; w[15] = q3.w;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = bswap4(ld16(p + 16 * q));
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
     } else if (b < total) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t o = 64 * b + 4 * k;
-        uint32_t v;
-        if (o + 4 <= L0) v = bswap32(*reinterpret_cast<const uint32_t *>(rec + o));
-        else if (esn && o == L0) v = esn_hi;
-        else if (o == L) v = 0x80000000u;
-        else v = 0;
-        if (b == total - 1 && k == 14) v = (uint32_t)(bits >> 32);
-        if (b == total - 1 && k == 15) v = (uint32_t)bits;
-        w[k] = v;
-      }
+      for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
     } else {
-      // outer: opad state, block = inner digest || 0x80 || 0... || (64+20)*8
+      outer_block<HS>(h, w);
 #pragma unroll
-      for (int k = 0; k < 5; ++k) w[k] = h[k];
-      w[5] = 0x80000000u;
-#pragma unroll
-      for (int k = 6; k < 15; ++k) w[k] = 0;
-      w[15] = (64 + 20) * 8;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) h[k] = opad[k];
+      for (int k = 0; k < W; ++k) h[k] = opad[k];
     }
-    sha1_compress(h, w);
+    Hash<HS>::compress(h, w);
   }
-  for (int k = 0; k < 5; ++k) out[k] = h[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = h[k];
 }
 
 __device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
 
 // One pass over an ETA record for the out-of-place decrypt: the record is
 // read once, in 64-byte HMAC chunks (lane = record); each chunk feeds the
-// SHA-1 compression AND the CBC decryption of the CT blocks it completes, so
-// the ciphertext is not fetched a second time for the cipher.  ESP places CT
-// block i at 24 + 16i: chunk 0 holds the IV (C_-1) and blocks 0, 1; chunk
-// b >= 1 holds the 8-byte tail of block 4b-2 and blocks 4b-1 .. 4b+1, whose
-// other 8 bytes came at the end of chunk b-1 (carried in two registers).
+// hash compression AND the decryption of the cipher blocks it completes, so
+// the ciphertext is not fetched a second time for the cipher.
+//  CBC (hlen 24): chunk 0 holds the IV (C_-1) and blocks 0, 1; chunk b >= 1
+//    holds the 8-byte tail of block 4b-2 and blocks 4b-1 .. 4b+1, whose other
+//    8 bytes came at the end of chunk b-1 (carried in two registers).
+//  CTR (hlen 16): chunk 0 holds the IV and blocks 0..2; chunk b >= 1 holds
+//    blocks 4b-1 .. 4b+2.  Keystream = AES_K(nonce || IV || be32(i+1)).
 // The <= 4 blocks after the last full chunk are decrypted on the way through
 // the first partial chunk.  Writes plaintext to out (MODE 0 decrypts records
 // whose ICV fails too; the status byte says so, as in the GCM kernel).
 // Returns whether the first mlen bytes of the HMAC match the ICV; *trl gets
 // the esp_input_cb trailer word from the last block.
-__device__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *orec, uint32_t plen, uint32_t mlen, bool esn,
-                                  uint32_t esn_hi, kptr ipad, kptr opad, kptr dk, int nr, const uint8_t *lds,
-                                  uint32_t slot, bool act, uint32_t *trl) {
-  const uint32_t L0 = 24 + plen, L = L0 + (esn ? 4u : 0u);
-  const uint32_t nfull = L0 / 64, total = (L + 9 + 63) / 64, nblk = plen / 16;
+template <int CK, int HS>
+__device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *orec, uint32_t plen, uint32_t mlen, bool esn,
+                                  uint32_t esn_hi, uint32_t salt, kptr ipad, kptr opad, kptr key, int nr,
+                                  const uint8_t *lds, uint32_t slot, bool act, uint32_t *trl) {
+  constexpr int W = Hash<HS>::W;
+  constexpr uint32_t HL = CK == CK_CBC ? 24u : 16u;
+  const uint32_t L0 = HL + plen, L = L0 + (esn ? 4u : 0u);
+  const uint32_t nfull = L0 / 64, total = (L + 9 + 63) / 64, nct = (plen + 15) / 16;
   const uint64_t bits = (uint64_t)(64 + L) * 8;
+  const uint8_t *te = lds + LDS_TE;
   uint32_t T = act ? total : 0;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) T = max(T, (uint32_t)__shfl_xor((int)T, o));
-  uint32_t h[5] = {ipad[0], ipad[1], ipad[2], ipad[3], ipad[4]};
+  uint32_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = k < W ? ipad[k] : 0u;
   uint4 prev = make_uint4(0, 0, 0, 0);
-  uint32_t cy0 = 0, cy1 = 0;
+  uint32_t cy0 = 0, cy1 = 0;                // CBC carry / CTR explicit IV
   for (uint32_t b = 0; b <= T; ++b) {
     const bool on = act && b <= total;
     uint32_t w[16];
-    uint32_t m[16];
     if (on && b < nfull) {
+      uint32_t m[16];
       const uint8_t *q = rec + 64 * b;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint4 v = ld16(q + 16 * k);
         m[4 * k] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
       }
-      uint4 blk[4];
-      int i0, nb;
-      if (b == 0) {                       // wave-uniform: every lane is at chunk 0 together
-        prev = make_uint4(m[2], m[3], m[4], m[5]);
-        blk[0] = make_uint4(m[6], m[7], m[8], m[9]);
-        blk[1] = make_uint4(m[10], m[11], m[12], m[13]);
-        blk[2] = blk[3] = make_uint4(0, 0, 0, 0);
-        i0 = 0;
-        nb = 2;
-      } else {
-        blk[0] = make_uint4(cy0, cy1, m[0], m[1]);
-        blk[1] = make_uint4(m[2], m[3], m[4], m[5]);
-        blk[2] = make_uint4(m[6], m[7], m[8], m[9]);
-        blk[3] = make_uint4(m[10], m[11], m[12], m[13]);
-        i0 = 4 * (int)b - 2;
-        nb = 4;
-      }
-      cy0 = m[14];
-      cy1 = m[15];
-      uint4 d[4] = {blk[0], blk[1], blk[2], blk[3]};
-      aes_dec4(d, dk, nr, lds, slot);
+      if (CK == CK_CBC) {
+        uint4 blk[4];
+        int i0, nb;
+        if (b == 0) {                       // wave-uniform: every lane is at chunk 0 together
+          prev = make_uint4(m[2], m[3], m[4], m[5]);
+          blk[0] = make_uint4(m[6], m[7], m[8], m[9]);
+          blk[1] = make_uint4(m[10], m[11], m[12], m[13]);
+          blk[2] = blk[3] = make_uint4(0, 0, 0, 0);
+          i0 = 0;
+          nb = 2;
+        } else {
+          blk[0] = make_uint4(cy0, cy1, m[0], m[1]);
+          blk[1] = make_uint4(m[2], m[3], m[4], m[5]);
+          blk[2] = make_uint4(m[6], m[7], m[8], m[9]);
+          blk[3] = make_uint4(m[10], m[11], m[12], m[13]);
+          i0 = 4 * (int)b - 2;
+          nb = 4;
+        }
+        cy0 = m[14];
+        cy1 = m[15];
+        uint4 d[4] = {blk[0], blk[1], blk[2], blk[3]};
+        aes_dec4(d, key, nr, lds, slot);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k < nb) {
-          st16(orec + 24 + 16 * (i0 + k), xor4(d[k], prev));
-          prev = blk[k];
+        for (int k = 0; k < 4; ++k) {
+          if (k < nb) {
+            st16(orec + HL + 16 * (i0 + k), xor4(d[k], prev));
+            prev = blk[k];
+          }
+        }
+      } else {
+        if (b == 0) {
+          cy0 = m[2];
+          cy1 = m[3];
+        }
+        uint4 ks[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ks[k] = make_uint4(salt, cy0, cy1, bswap32(4 * b + (uint32_t)k));
+        aes_enc4(ks, key, nr, te, slot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (b > 0 || k > 0)               // chunk 0 starts with SPI|SN|IV
+            st16(orec + HL + 16 * (4 * b - 1 + (uint32_t)k),
+                 xor4(make_uint4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]), ks[k]));
         }
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = bswap32(m[k]);
     } else if (on && b < total) {
       if (b == nfull) {
-        // the CT blocks after the last full chunk (1..4 of them)
-        const int i0 = nfull == 0 ? 0 : 4 * (int)nfull - 2;
-        if (nfull == 0) prev = ld16(rec + 8);
-        uint4 blk[4], d[4];
+        // the cipher blocks after the last full chunk (1..4 of them)
+        if (CK == CK_CBC) {
+          const int i0 = nfull == 0 ? 0 : 4 * (int)nfull - 2;
+          if (nfull == 0) prev = ld16(rec + 8);
+          uint4 blk[4], d[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          blk[k] = make_uint4(0, 0, 0, 0);
-          if (i0 + k < (int)nblk) blk[k] = ld16(rec + 24 + 16 * (i0 + k));
-          d[k] = blk[k];
-        }
-        aes_dec4(d, dk, nr, lds, slot);
+          for (int k = 0; k < 4; ++k) {
+            blk[k] = make_uint4(0, 0, 0, 0);
+            if (i0 + k < (int)nct) blk[k] = ld16(rec + HL + 16 * (i0 + k));
+            d[k] = blk[k];
+          }
+          aes_dec4(d, key, nr, lds, slot);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (i0 + k < (int)nblk) {
-            const uint4 pt = xor4(d[k], prev);
-            st16(orec + 24 + 16 * (i0 + k), pt);
-            if (i0 + k == (int)nblk - 1) *trl = esp_trailer_word(pt.w, plen);
-            prev = blk[k];
+          for (int k = 0; k < 4; ++k) {
+            if (i0 + k < (int)nct) {
+              const uint4 pt = xor4(d[k], prev);
+              st16(orec + HL + 16 * (i0 + k), pt);
+              if (i0 + k == (int)nct - 1) *trl = esp_trailer_word(pt.w, plen);
+              prev = blk[k];
+            }
+          }
+        } else {
+          const int i0 = nfull == 0 ? 0 : 4 * (int)nfull - 1;
+          if (nfull == 0) {
+            cy0 = *reinterpret_cast<const uint32_t *>(rec + 8);
+            cy1 = *reinterpret_cast<const uint32_t *>(rec + 12);
+          }
+          uint4 c[4], ks[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            c[k] = make_uint4(0, 0, 0, 0);
+            if (i0 + k < (int)nct) c[k] = ld16(rec + HL + 16 * (i0 + k));
+            ks[k] = make_uint4(salt, cy0, cy1, bswap32((uint32_t)(i0 + k) + 1u));
+          }
+          aes_enc4(ks, key, nr, te, slot);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (i0 + k < (int)nct) {
+              const int rem = (int)plen - 16 * (i0 + k);
+              const uint4 pt = xor4(c[k], ks[k]);
+              st_partial(orec + HL + 16 * (i0 + k), pt, rem);
+              if (i0 + k == (int)nct - 1) *trl = esp_trailer_word(last_word(pt, rem), plen);
+            }
           }
         }
       }
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t o = 64 * b + 4 * k;
-        uint32_t v;
-        if (o + 4 <= L0) v = bswap32(*reinterpret_cast<const uint32_t *>(rec + o));
-        else if (esn && o == L0) v = esn_hi;
-        else if (o == L) v = 0x80000000u;
-        else v = 0;
-        if (b == total - 1 && k == 14) v = (uint32_t)(bits >> 32);
-        if (b == total - 1 && k == 15) v = (uint32_t)bits;
-        w[k] = v;
-      }
+      for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
     } else {
-#pragma unroll
-      for (int k = 0; k < 5; ++k) w[k] = h[k];
-      w[5] = 0x80000000u;
-#pragma unroll
-      for (int k = 6; k < 15; ++k) w[k] = 0;
-      w[15] = (64 + 20) * 8;
+      outer_block<HS>(h, w);
       if (on) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) h[k] = opad[k];
+        for (int k = 0; k < W; ++k) h[k] = opad[k];
       }
     }
-    uint32_t hn[5] = {h[0], h[1], h[2], h[3], h[4]};
-    sha1_compress(hn, w);
+    uint32_t hn[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hn[k] = h[k];
+    Hash<HS>::compress(hn, w);
     if (on) {
 #pragma unroll
-      for (int k = 0; k < 5; ++k) h[k] = hn[k];
+      for (int k = 0; k < W; ++k) h[k] = hn[k];
     }
   }
   uint32_t diff = 0;
@@ -421,19 +601,51 @@ __device__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *orec, uint32_t pl
   return act && diff == 0;
 }
 
-// MODE 0: decrypt out-of-place; 1: encrypt in place; 2: decrypt in place (verify first)
-template <int MODE, int WG>
-__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t slot = (uint32_t)(lane & 31) * 4;
-  const uint2 *tab = MODE == 1 ? p.tpair : p.dpair;
-  for (int idx = tid; idx < 256 * 32; idx += WG) {
+template <int CK>
+__device__ __forceinline__ bool fused_hs(int aalg, const uint8_t *rec, uint8_t *orec, uint32_t plen,
+                                         uint32_t mlen, bool esn, uint32_t esn_hi, uint32_t salt, kptr ipad,
+                                         kptr opad, kptr key, int nr, const uint8_t *lds, uint32_t slot, bool act,
+                                         uint32_t *trl) {
+  if (aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+    return eta_decrypt_fused<CK, HS_SHA256>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds,
+                                            slot, act, trl);
+  return eta_decrypt_fused<CK, HS_SHA1>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds, slot,
+                                        act, trl);
+}
+
+__device__ __forceinline__ void hmac_any(int aalg, const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi,
+                                         kptr ipad, kptr opad, uint32_t out[8]) {
+  if (aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+    hmac_t<HS_SHA256>(rec, L0, esn, esn_hi, ipad, opad, out);
+  else
+    hmac_t<HS_SHA1>(rec, L0, esn, esn_hi, ipad, opad, out);
+}
+
+__device__ __forceinline__ void fill_pair(uint8_t *lds, uint32_t base, const uint2 *tab, int tid, int wg) {
+  for (int idx = tid; idx < 256 * 32; idx += wg) {
     const int x = idx >> 5, r = idx & 31;
     const uint2 t = tab[x];
-    *reinterpret_cast<uint32_t *>(lds + LDS_T + x * 256 + r * 4) = t.x;
-    *reinterpret_cast<uint32_t *>(lds + LDS_T + x * 256 + 128 + r * 4) = t.y;
-    if (MODE != 1) *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[x];
+    *reinterpret_cast<uint32_t *>(lds + base + x * 256 + r * 4) = t.x;
+    *reinterpret_cast<uint32_t *>(lds + base + x * 256 + 128 + r * 4) = t.y;
+  }
+}
+
+// MODE 0: decrypt out-of-place; 1: encrypt in place; 2: decrypt in place (verify first)
+// CKS: MODE 0 is built once per cipher (CK_CBC / CK_CTR) and each launch
+// serves only its cipher's sessions -- both fused paths inlined in one kernel
+// made the register allocator spill; -1 = every ETA session.
+template <int MODE, int WG, int CKS>
+__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t slot = (uint32_t)(lane & 31) * 4;
+  if (MODE == 1) {
+    fill_pair(lds, LDS_T, p.tpair, tid, WG);
+  } else {
+    fill_pair(lds, LDS_T, p.dpair, tid, WG);
+    fill_pair(lds, LDS_TE, p.tpair, tid, WG);
+    for (int idx = tid; idx < 256 * 32; idx += WG)
+      *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[idx >> 5];
   }
   __syncthreads();
 
@@ -460,12 +672,14 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
     }
     // ---- lane = record: descriptor, HMAC (verify or compute) ----
     bool valid = false, ok = false;
-    uint32_t off = 0, len = 0, sa = 0, plen = 0;
+    uint32_t off = 0, len = 0, sa = 0, plen = 0, hl = 24, salt = 0, esnh = 0;
     if (have) {
       const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
       off = dv.x * 4;
       len = dv.y & 0xffffu;
       sa = dv.y >> 16;
+      esnh = dv.z;
+      salt = dv.w;
       const DevSA *s = sa < p.nsas ? p.sas + sa : nullptr;
       if (!s || s->mode != ESPGPU_CSP_MODE_ETA) {
         have = false;                                       // not ours (GCM kernel / EINVAL)
@@ -473,40 +687,56 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           p.status[di] = ESPGPU_EINVAL;
           if (MODE != 1 && p.trailer) p.trailer[di] = 0;
         }
+      } else if (CKS >= 0 && (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR)) {
+        have = false;                                       // the other cipher's launch
       } else {
+        const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;
         const uint32_t mlen = s->mlen;
-        const int pl = (int)len - 24 - (int)mlen;           // hlen 24, alen = mlen (12)
-        valid = pl > 0 && (pl & 15) == 0 && (len & 3) == 0;  // xform_esp.c:316-324
+        hl = ctr ? 16u : 24u;                               // SPI|SN|IV8 or SPI|SN|IV16
+        const int pl = (int)len - (int)hl - (int)mlen;      // alen = mlen
+        // xform_esp.c:316-324: payload > 0 and a multiple of the cipher's
+        // blocksize (16 for CBC, 1 for CTR; records are 4-byte multiples)
+        valid = pl > 0 && (ctr || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
         if (valid && MODE == 2) {
-          uint32_t dg[5];
+          uint32_t dg[8];
           const uint8_t *rec = p.arena + off;
-          hmac_sha1(rec, 24 + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, dv.z, kp(s->ipad),
-                    kp(s->opad), dg);
+          hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                   kp(s->opad), dg);
           uint32_t diff = 0;
           for (uint32_t k = 0; k < mlen / 4; ++k)
-            diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + 24 + plen + 4 * k);
+            diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
           ok = diff == 0;
         }
       }
     }
     if (MODE == 1) {
-      // ---- encrypt: CBC chain is serial, lane = record ----
+      // ---- encrypt: lane = record (the CBC chain is serial; CTR uses the
+      // same loop with independent blocks) ----
       if (have && valid) {
         const DevSA *s = p.sas + sa;
         uint8_t *rec = p.arena + off;
-        uint4 prev = ld16(rec + 8);                         // IV
         const int nr = (int)s->nr;
-        for (uint32_t b = 0; b < plen / 16; ++b) {
-          const uint4 c = aes_enc(xor4(ld16(rec + 24 + 16 * b), prev), s->rk, nr, lds, slot);
-          st16(rec + 24 + 16 * b, c);
-          prev = c;
+        if (s->calg == ESPGPU_CRYPTO_AES_ICM) {
+          const uint32_t iv0 = *reinterpret_cast<const uint32_t *>(rec + 8);
+          const uint32_t iv1 = *reinterpret_cast<const uint32_t *>(rec + 12);
+          for (uint32_t b = 0; b < (plen + 15) / 16; ++b) {
+            const uint4 ks = aes_enc(make_uint4(salt, iv0, iv1, bswap32(b + 1)), s->rk, nr, lds, slot);
+            st_partial(rec + 16 + 16 * b, xor4(ld16(rec + 16 + 16 * b), ks), (int)(plen - 16 * b));
+          }
+        } else {
+          uint4 prev = ld16(rec + 8);                       // IV
+          for (uint32_t b = 0; b < plen / 16; ++b) {
+            const uint4 c = aes_enc(xor4(ld16(rec + 24 + 16 * b), prev), s->rk, nr, lds, slot);
+            st16(rec + 24 + 16 * b, c);
+            prev = c;
+          }
         }
-        uint32_t dg[5];
-        hmac_sha1(rec, 24 + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, p.desc[di].esn_hi,
-                  kp(s->ipad), kp(s->opad), dg);
+        uint32_t dg[8];
+        hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                 kp(s->opad), dg);
         for (uint32_t k = 0; k < s->mlen / 4; ++k)
-          *reinterpret_cast<uint32_t *>(rec + 24 + plen + 4 * k) = bswap32(dg[k]);
+          *reinterpret_cast<uint32_t *>(rec + hl + plen + 4 * k) = bswap32(dg[k]);
       }
       if (have) p.status[di] = valid ? ESPGPU_OK : ESPGPU_EINVAL;
       continue;
@@ -523,10 +753,10 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         run = run && !mine;
         const DevSA *s = p.sas + sau;
         uint32_t trl = 0;
-        const bool good = eta_decrypt_fused(p.arena + off, p.out + off, plen, s->mlen,
-                                            (s->flags & ESPGPU_CSP_F_ESN) != 0, mine ? p.desc[di].esn_hi : 0,
-                                            kp(s->ipad), kp(s->opad), kp(s->dk), (int)s->nr, lds, slot, mine,
-                                            &trl);
+        const bool esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
+        const bool good = fused_hs<CKS == CK_CTR ? CK_CTR : CK_CBC>(
+            (int)s->aalg, p.arena + off, p.out + off, plen, s->mlen, esn, esnh, salt, kp(s->ipad), kp(s->opad),
+            kp(CKS == CK_CTR ? s->rk : s->dk), (int)s->nr, lds, slot, mine, &trl);
         if (mine) {
           ok = good;
           if (p.trailer) p.trailer[di] = good ? trl : 0u;
@@ -541,21 +771,24 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
     // decrypting a record's last block writes the others'
     if (have && p.trailer && !(valid && ok)) p.trailer[di] = 0;
 
-    // ---- decrypt: all of the wave's blocks of one session as one flat list ----
+    // ---- verified in-place decrypt: all of the wave's blocks of one session
+    // as one flat list ----
     // Records to decrypt (one session at a time, so the round keys stay
-    // wave-uniform in SGPRs: one pass for planner chunks) are concatenated;
-    // every lane takes one block per pass, last pass first.  Within a pass all
-    // lanes load C_i and C_{i-1} before any lane stores, and a pass only
-    // overwrites blocks no later (lower) pass reads: in-place decryption is
-    // safe without holding records in registers.
-    bool run = have && valid && (MODE == 0 || ok);
+    // wave-uniform in SGPRs) are concatenated; every lane takes one block per
+    // pass, last pass first.  Within a pass all lanes load their blocks (and
+    // C_{i-1}) before any lane stores, and a pass only overwrites blocks no
+    // later (lower) pass reads: in-place decryption is safe without holding
+    // records in registers.
+    bool run = have && valid && ok;
     uint64_t todo = __ballot(run);
     while (todo) {
       const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
       const bool mine = run && sa == sau;
       todo &= ~__ballot(mine);
       run = run && !mine;
-      const uint32_t nb = mine ? plen / 16 : 0;
+      const DevSA *s = p.sas + sau;
+      const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;      // wave-uniform
+      const uint32_t nb = mine ? (plen + 15) / 16 : 0;
       uint32_t incl = nb;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -564,10 +797,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       }
       const uint32_t start = incl - nb;
       const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
-      const DevSA *s = p.sas + sau;
       const int nr = (int)s->nr;
-      const kptr dk = kp(s->dk);
-      uint8_t *const obase = MODE == 0 ? p.out : p.arena;
       for (int base = total - 64; base > -64; base -= 64) {
         const int f = base + lane;
         // the record holding flat block f: the last lane whose start <= f
@@ -582,16 +812,25 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           }
         }
         const uint32_t ro = __shfl(off, j);
-        const uint32_t rpl = __shfl(plen, j), rdi = __shfl(di, j);
-        const int rok = __shfl((int)ok, j);        // MODE 0 also decrypts failed records
+        const uint32_t rpl = __shfl(plen, j), rdi = __shfl(di, j), rsalt = __shfl(salt, j);
         if (f >= 0) {
           const uint32_t i = (uint32_t)f - sj;
-          const uint8_t *rec = p.arena + ro;
-          const uint4 c = ld16(rec + 24 + 16 * i);
-          const uint4 prev = ld16(rec + 8 + 16 * i);         // C_{i-1}, or the IV for i = 0
-          const uint4 pt = xor4(aes_dec(c, dk, nr, lds, slot), prev);
-          st16(obase + ro + 24 + 16 * i, pt);
-          if (p.trailer && i == rpl / 16 - 1 && rok) p.trailer[rdi] = esp_trailer_word(pt.w, rpl);
+          uint8_t *rec = p.arena + ro;
+          const int rem = (int)rpl - 16 * (int)i;
+          uint4 pt;
+          if (ctr) {
+            const uint4 c = ld16(rec + 16 + 16 * i);
+            const uint4 cb = make_uint4(rsalt, *reinterpret_cast<const uint32_t *>(rec + 8),
+                                        *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(i + 1));
+            pt = xor4(c, aes_enc(cb, kp(s->rk), nr, lds + LDS_TE, slot));
+            st_partial(rec + 16 + 16 * i, pt, rem);
+          } else {
+            const uint4 c = ld16(rec + 24 + 16 * i);
+            const uint4 prev = ld16(rec + 8 + 16 * i);       // C_{i-1}, or the IV for i = 0
+            pt = xor4(aes_dec(c, kp(s->dk), nr, lds, slot), prev);
+            st16(rec + 24 + 16 * i, pt);
+          }
+          if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdi] = esp_trailer_word(last_word(pt, rem), rpl);
         }
       }
     }
@@ -606,24 +845,26 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 
 }  // namespace
 
-// Decrypt runs 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the
-// unrolled SHA-1 schedule needs ~150 and spills at 128), one workgroup per CU
-// (96 KiB LDS); encrypt runs 1024.
-int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream) {
+// 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
+// schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   // implicit units (64 records, one wave each): no more workgroups than units
   if (p.chunks == nullptr) {
-    const int units = (int)((p.n + 63) / 64), wpg = (encrypt ? 1024 : 768) / 64;
+    const int units = (int)((p.n + 63) / 64), wpg = 768 / 64;
     grid = std::max(1, std::min(grid, (units + wpg - 1) / wpg));
   }
   const int two_pass = !encrypt && p.out == p.arena;
-  if (encrypt)
-    hipLaunchKernelGGL((eta_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, p);
-  else if (two_pass)
-    hipLaunchKernelGGL((eta_kernel<2, 768>), dim3(grid), dim3(768), 0, st, p);
-  else
-    hipLaunchKernelGGL((eta_kernel<0, 768>), dim3(grid), dim3(768), 0, st, p);
+  if (encrypt) {
+    hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(grid), dim3(768), 0, st, p);
+  } else if (two_pass) {
+    hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(grid), dim3(768), 0, st, p);
+  } else {
+    // kinds: bit 0 = CBC sessions exist, bit 1 = CTR sessions exist
+    if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(grid), dim3(768), 0, st, p);
+    if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(grid), dim3(768), 0, st, p);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -33,6 +33,7 @@ constexpr uint32_t kSmallBatchBytes = 128u << 10;
 struct Session {
   bool used = false;
   int mode = 0, flags = 0, mlen = 0, klen = 0;
+  bool ctr = false;       // ETA with AES-ICM (RFC 3686 ESP AES-CTR)
 };
 
 struct Pending {
@@ -93,7 +94,7 @@ struct espgpu_ctx {
   uint32_t *d_queue = nullptr;   // work queues: [0..1] GCM, [2..3] ETA (ticket, retired; self-resetting)
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
-  int n_eta = 0;
+  int n_eta = 0, n_ctr = 0;   // ETA sessions, of which AES-CTR
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -264,7 +265,8 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.isbox = c->d_isbox;
     q.status = d_status;
     q.nsas = nsas;
-    if (launch_eta(q, encrypt, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
+    const int ek = (c->n_eta - c->n_ctr > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0);
+    if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
   c->last_st = st;
@@ -387,13 +389,20 @@ int espgpu_probesession(const espgpu_session_params *csp) {
       if (csp->csp_auth_mlen > 16 || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
       if (csp->csp_flags & ESPGPU_CSP_F_ESN) return ESPGPU_EINVAL;    // ESN for GCM = SEPARATE_AAD
       return ESPGPU_PROBE_HARDWARE;
-    case ESPGPU_CSP_MODE_ETA:
-      if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC || !aes_klen) return ESPGPU_EINVAL;
+    case ESPGPU_CSP_MODE_ETA: {
+      // AES-CBC or AES-ICM (CTR; csp_ivlen = the enc_xform's 16, the nonce
+      // rides in crp_iv) with HMAC-SHA1 or HMAC-SHA2-256 (esp_init :225-241)
+      if ((csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC && csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_ICM) ||
+          !aes_klen)
+        return ESPGPU_EINVAL;
       if (csp->csp_ivlen != 16) return ESPGPU_EINVAL;
-      if (csp->csp_auth_alg != ESPGPU_CRYPTO_SHA1_HMAC || csp->csp_auth_klen <= 0) return ESPGPU_EINVAL;
-      if (csp->csp_auth_mlen > 20 || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
+      const int hashlen = csp->csp_auth_alg == ESPGPU_CRYPTO_SHA1_HMAC ? 20
+                        : csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_256_HMAC ? 32 : 0;
+      if (!hashlen || csp->csp_auth_klen <= 0) return ESPGPU_EINVAL;
+      if (csp->csp_auth_mlen > hashlen || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
       if (csp->csp_flags & ESPGPU_CSP_F_SEPARATE_AAD) return ESPGPU_EINVAL;
       return ESPGPU_PROBE_HARDWARE;
+    }
     default:
       return ESPGPU_EINVAL;
   }
@@ -433,14 +442,25 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     hc::ghash_tables(h, kGcmLanesPerRec, tabs.data());
     HIPCHK(c, hipMemcpy(c->d_gtab + (size_t)slot * kGhTableBytes, tabs.data(), kGhTableBytes, hipMemcpyHostToDevice));
   } else {
-    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : 20;
+    const bool sha256 = csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_256_HMAC;
+    sa.calg = (uint32_t)csp->csp_cipher_alg;
+    sa.aalg = (uint32_t)csp->csp_auth_alg;
+    // mlen 0 = the whole hash (swcr_setup_auth, cryptosoft.c:1013-1018)
+    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : (sha256 ? 32u : 20u);
     for (int i = 0; i < 4 * (nr + 1); ++i) sa.rk[i] = rk[i];
     uint32_t dk[60];
     hc::aes_expand_dec(key, csp->csp_cipher_klen, dk);
     for (int i = 0; i < 4 * (nr + 1); ++i) sa.dk[i] = dk[i];
-    hc::hmac_sha1_pad_state((const uint8_t *)csp->csp_auth_key, csp->csp_auth_klen, 0x36, sa.ipad);
-    hc::hmac_sha1_pad_state((const uint8_t *)csp->csp_auth_key, csp->csp_auth_klen, 0x5c, sa.opad);
+    const uint8_t *ak = (const uint8_t *)csp->csp_auth_key;
+    if (sha256) {
+      hc::hmac_sha256_pad_state(ak, csp->csp_auth_klen, 0x36, sa.ipad);
+      hc::hmac_sha256_pad_state(ak, csp->csp_auth_klen, 0x5c, sa.opad);
+    } else {
+      hc::hmac_sha1_pad_state(ak, csp->csp_auth_klen, 0x36, sa.ipad);
+      hc::hmac_sha1_pad_state(ak, csp->csp_auth_klen, 0x5c, sa.opad);
+    }
     c->n_eta++;
+    if (csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM) c->n_ctr++;
   }
   HIPCHK(c, hipMemcpy(c->d_sas + slot, &sa, sizeof sa, hipMemcpyHostToDevice));
   Session &s = c->sessions[slot];
@@ -449,6 +469,7 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   s.flags = csp->csp_flags;
   s.mlen = (int)sa.mlen;
   s.klen = csp->csp_cipher_klen;
+  s.ctr = csp->csp_mode == ESPGPU_CSP_MODE_ETA && csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
   c->h_sas[slot] = sa;
   *sid_out = slot;
   return 0;
@@ -463,6 +484,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   hipStreamSynchronize(c->s_out);
   for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
   if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
+  if (c->sessions[sid].ctr) c->n_ctr--;
   c->sessions[sid] = Session();
   DevSA z;
   memset(&z, 0, sizeof z);
@@ -495,8 +517,8 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   for (int i = 0; i < r->nsegs; ++i) total += r->segs[i].len;
   const bool gcm = ses.mode == ESPGPU_CSP_MODE_AEAD;
   // ICV bytes in the record: the session's (possibly truncated) mlen, 16/12/8
-  // for GCM (cryptosoft.c:1112-1117), 12 or 20 for HMAC-SHA1
-  const int ivlen = gcm ? 8 : 16, hlen = 8 + ivlen, alen = ses.mlen;
+  // for GCM (cryptosoft.c:1112-1117), 12 or 20 for HMAC-SHA1, 16 for HMAC-SHA2-256-128
+  const int ivlen = (gcm || ses.ctr) ? 8 : 16, hlen = 8 + ivlen, alen = ses.mlen;
   const int plen = r->crp_payload_length;
   int aad_start = r->crp_aad_start;
   // ESP shape checks
@@ -518,6 +540,19 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
       if (!seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)aad_start, 8, hdr)) return reject(ESPGPU_EINVAL);
     }
     salt = le32(r->crp_iv);
+  } else if (ses.ctr) {
+    // AES-CTR: crp_iv = nonce || explicit IV || be32(1) (xform_esp.c:453-458),
+    // and the explicit IV is the record's; the kernel rebuilds the counter
+    // blocks from the descriptor's salt (the nonce) and the record
+    if (!(r->crp_flags & ESPGPU_CRYPTO_F_IV_SEPARATE) || r->crp_aad || r->crp_aad_length != hlen ||
+        r->crp_payload_start != aad_start + hlen || be32(r->crp_iv + 12) != 1u)
+      return reject(ESPGPU_EINVAL);
+    uint8_t ivb[8];
+    if (!seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)(aad_start + 8), 8, ivb) ||
+        memcmp(ivb, r->crp_iv + 4, 8) != 0)
+      return reject(ESPGPU_EINVAL);
+    salt = le32(r->crp_iv);
+    if (ses.flags & ESPGPU_CSP_F_ESN) esn_hi = be32(r->crp_esn);
   } else {
     if (r->crp_aad || r->crp_aad_length != hlen || r->crp_iv_start != aad_start + 8 ||
         r->crp_payload_start != aad_start + hlen || (plen & 15))

@@ -23,9 +23,11 @@ struct DevSA {
   uint32_t mode;    // ESPGPU_CSP_MODE_AEAD / _ETA, 0 = free slot
   uint32_t flags;   // csp_flags
   uint32_t mlen;    // ICV bytes compared / written
-  uint32_t ipad[5];
-  uint32_t opad[5];
-  uint32_t pad_[256 - 128 - 4 - 10];
+  uint32_t ipad[8]; // ETA: HMAC chaining states after the ipad / opad key
+  uint32_t opad[8]; //      block (5 words SHA-1, 8 words SHA2-256)
+  uint32_t calg;    // ETA cipher: ESPGPU_CRYPTO_AES_CBC or _AES_ICM (CTR)
+  uint32_t aalg;    // ETA auth: ESPGPU_CRYPTO_SHA1_HMAC or _SHA2_256_HMAC
+  uint32_t pad_[256 - 128 - 4 - 16 - 2];
 };
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 
@@ -108,7 +110,8 @@ __host__ __device__ inline uint32_t esp_trailer_word(uint32_t wlast, uint32_t pl
 // Launchers (defined in the .hip files, called by espgpu.cpp).
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream);
 int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
-int launch_eta(const EtaParams &p, int encrypt, int grid, void *stream);
+// kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream);

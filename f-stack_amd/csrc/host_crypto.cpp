@@ -236,5 +236,69 @@ void hmac_sha1_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t 
   sha1_compress(h, k);
 }
 
+// SHA-256 (FIPS 180-4; freebsd/crypto/sha2/sha256c.c SHA256_Transform :135)
+static const uint32_t K256[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u,
+};
+static inline uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+void sha256_compress(uint32_t h[8], const uint8_t blk[64]) {
+  uint32_t w[64], v[8];
+  for (int i = 0; i < 16; ++i) w[i] = be32(blk + 4 * i);
+  for (int i = 16; i < 64; ++i) {
+    const uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    const uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  for (int i = 0; i < 8; ++i) v[i] = h[i];
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t t1 = v[7] + (rotr32(v[4], 6) ^ rotr32(v[4], 11) ^ rotr32(v[4], 25)) +
+                        ((v[4] & v[5]) ^ (~v[4] & v[6])) + K256[i] + w[i];
+    const uint32_t t2 = (rotr32(v[0], 2) ^ rotr32(v[0], 13) ^ rotr32(v[0], 22)) +
+                        ((v[0] & v[1]) ^ (v[0] & v[2]) ^ (v[1] & v[2]));
+    v[7] = v[6]; v[6] = v[5]; v[5] = v[4]; v[4] = v[3] + t1;
+    v[3] = v[2]; v[2] = v[1]; v[1] = v[0]; v[0] = t1 + t2;
+  }
+  for (int i = 0; i < 8; ++i) h[i] += v[i];
+}
+
+static const uint32_t kSha256Iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                      0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+static void sha256_full(const uint8_t *m, int len, uint8_t out[32]) {
+  uint32_t h[8];
+  memcpy(h, kSha256Iv, sizeof h);
+  int off = 0;
+  for (; len - off >= 64; off += 64) sha256_compress(h, m + off);
+  uint8_t tail[128] = {0};
+  const int rem = len - off;
+  memcpy(tail, m + off, (size_t)rem);
+  tail[rem] = 0x80;
+  const int tl = (rem + 9 <= 64) ? 64 : 128;
+  const uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+  sha256_compress(h, tail);
+  if (tl == 128) sha256_compress(h, tail + 64);
+  for (int i = 0; i < 8; ++i) put_be32(out + 4 * i, h[i]);
+}
+
+// hmac_init_pad (crypto.c:413-441) for HMAC-SHA2-256: the chaining state
+// after the padded key block (the key is hashed first when longer than 64)
+void hmac_sha256_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t h[8]) {
+  uint8_t k[64] = {0};
+  if (klen > 64) sha256_full(key, klen, k);
+  else if (klen > 0) memcpy(k, key, (size_t)klen);
+  for (int i = 0; i < 64; ++i) k[i] ^= padval;
+  memcpy(h, kSha256Iv, 32);
+  sha256_compress(h, k);
+}
+
 }  // namespace hc
 }  // namespace espgpu

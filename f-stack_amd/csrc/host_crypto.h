@@ -33,6 +33,8 @@ void ghash_tables(const uint8_t h[16], int stride, uint8_t *out);
 void sha1_compress(uint32_t h[5], const uint8_t block[64]);
 // HMAC pad state: h = SHA1-compress(IV, (key or SHA1(key)) ^ padval).
 void hmac_sha1_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t h[5]);
+void sha256_compress(uint32_t h[8], const uint8_t block[64]);
+void hmac_sha256_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t h[8]);
 
 }  // namespace hc
 }  // namespace espgpu

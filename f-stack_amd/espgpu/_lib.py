@@ -18,6 +18,8 @@ CSP_F_SEPARATE_AAD = 0x2
 CSP_F_ESN = 0x4
 CRYPTO_SHA1_HMAC = 7
 CRYPTO_AES_CBC = 11
+CRYPTO_SHA2_256_HMAC = 18
+CRYPTO_AES_ICM = 23
 CRYPTO_AES_NIST_GCM_16 = 25
 CRYPTO_OP_DECRYPT = 0x0
 CRYPTO_OP_ENCRYPT = 0x1

@@ -13,6 +13,9 @@ from . import _lib as L
 from .opencrypto import crypto_session_params
 
 GCM, CBC_SHA1 = "aes-gcm-16", "aes-cbc-hmac-sha1-96"
+CBC_SHA256 = "aes-cbc-hmac-sha2-256-128"
+CTR_SHA1, CTR_SHA256 = "aes-ctr-hmac-sha1-96", "aes-ctr-hmac-sha2-256-128"   # RFC 3686
+ETA_ALGS = (CBC_SHA1, CBC_SHA256, CTR_SHA1, CTR_SHA256)
 IPPROTO_NONE = 59
 
 
@@ -25,13 +28,26 @@ class SecAssoc:
         self.key = bytes(key)          # GCM: cipher key || 4-byte salt (RFC 4106 8.1)
         self.auth_key = bytes(auth_key)
         self.esn = esn
-        # ICV bytes: xform_ah_authsize (GMAC 16, SHA1-HMAC 12); a GCM SA may
-        # carry a truncated 12- or 8-byte ICV (RFC 4106 s3.3, csp_auth_mlen)
-        self.mlen = mlen if mlen is not None else (16 if alg == GCM else 12)
+        # ICV bytes: xform_ah_authsize (GMAC 16, SHA1-HMAC 12, SHA2-256-HMAC
+        # 16 = hashsize/2); a GCM SA may carry a truncated 12- or 8-byte ICV
+        # (RFC 4106 s3.3, csp_auth_mlen)
+        self.mlen = mlen if mlen is not None else (12 if alg in (CBC_SHA1, CTR_SHA1) else 16)
+
+    @property
+    def ctr(self):
+        return self.alg in (CTR_SHA1, CTR_SHA256)
+
+    @property
+    def cipher_alg(self):
+        return L.CRYPTO_AES_ICM if self.ctr else L.CRYPTO_AES_CBC
+
+    @property
+    def auth_alg(self):
+        return L.CRYPTO_SHA2_256_HMAC if self.alg in (CBC_SHA256, CTR_SHA256) else L.CRYPTO_SHA1_HMAC
 
     @property
     def ivlen(self):
-        return 8 if self.alg == GCM else 16
+        return 8 if self.alg == GCM or self.ctr else 16       # RFC 4106 / 3686: 8-byte IV
 
     @property
     def hlen(self):
@@ -43,11 +59,12 @@ class SecAssoc:
 
     @property
     def blocksize(self):
-        return 1 if self.alg == GCM else 16   # enc_xform blocksize (ESP pads to 4 anyway)
+        return 16 if self.alg in (CBC_SHA1, CBC_SHA256) else 1   # enc_xform blocksize (ESP pads to 4 anyway)
 
     @property
     def salt(self):
-        return self.key[-4:] if self.alg == GCM else b"\0\0\0\0"
+        # the 4-byte salt / nonce esp_init strips off the key (RFC 4106 8.1, RFC 3686 5.1)
+        return self.key[-4:] if self.alg == GCM or self.ctr else b"\0\0\0\0"
 
     def csp(self):
         if self.alg == GCM:
@@ -57,11 +74,12 @@ class SecAssoc:
                 csp_ivlen=12, csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16,
                 csp_cipher_klen=len(self.key) - 4, csp_cipher_key=self.key[:-4],
                 csp_auth_mlen=0 if self.mlen == 16 else self.mlen)
+        ckey = self.key[:-4] if self.ctr else self.key
         return crypto_session_params(
             csp_mode=L.CSP_MODE_ETA, csp_flags=L.CSP_F_ESN if self.esn else 0,
-            csp_ivlen=16, csp_cipher_alg=L.CRYPTO_AES_CBC, csp_cipher_klen=len(self.key),
-            csp_cipher_key=self.key, csp_auth_alg=L.CRYPTO_SHA1_HMAC,
-            csp_auth_klen=len(self.auth_key), csp_auth_key=self.auth_key, csp_auth_mlen=12)
+            csp_ivlen=16, csp_cipher_alg=self.cipher_alg, csp_cipher_klen=len(ckey),
+            csp_cipher_key=ckey, csp_auth_alg=self.auth_alg,
+            csp_auth_klen=len(self.auth_key), csp_auth_key=self.auth_key, csp_auth_mlen=self.mlen)
 
 
 def _flat(buf):
@@ -88,8 +106,9 @@ def esp_input_crp(fw, ses, sa, pkt, skip, esn_hi=0):
     crp.crp_buf = pkt
     crp.crp_payload_start = skip + sa.hlen                                    # :424-425
     crp.crp_payload_length = total - (skip + sa.hlen + sa.alen)
-    if sa.alg == GCM:                                                         # :430-455
-        crp.crp_iv = bytearray(sa.salt + data[skip + sa.hlen - sa.ivlen:skip + sa.hlen] + b"\0" * 4)
+    if sa.alg == GCM or sa.ctr:                                               # :430-458
+        ctr0 = struct.pack(">I", 1) if sa.ctr else b"\0" * 4
+        crp.crp_iv = bytearray(sa.salt + data[skip + sa.hlen - sa.ivlen:skip + sa.hlen] + ctr0)
         crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
     else:
         crp.crp_iv_start = skip + sa.hlen - sa.ivlen
@@ -120,7 +139,11 @@ def esp_output_crp(fw, ses, sa, pkt, skip, esn_hi=0):
     else:
         crp.crp_aad_start = skip
         crp.crp_aad_length = sa.hlen
-        crp.crp_iv_start = skip + 8
+        if sa.ctr:
+            crp.crp_iv = bytearray(sa.salt + data[skip + 8:skip + 16] + struct.pack(">I", 1))
+            crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
+        else:
+            crp.crp_iv_start = skip + 8
         if sa.esn:
             crp.crp_esn = seqh
     return crp

@@ -6,7 +6,8 @@
  * framework, i.e. it replaces the software driver "cryptosoft"
  * (freebsd/opencrypto/cryptosoft.c) for the ESP ciphers F-Stack's IPsec uses:
  *   AES-GCM-16 (CSP_MODE_AEAD)                  -> swcr_gcm      cryptosoft.c:465-645
- *   AES-CBC + HMAC-SHA1-96 (CSP_MODE_ETA)       -> swcr_eta      cryptosoft.c:874-888
+ *   AES-CBC or AES-CTR (RFC 3686) + HMAC-SHA1-96
+ *     or HMAC-SHA2-256-128 (CSP_MODE_ETA)       -> swcr_eta      cryptosoft.c:874-888
  * Every entry point is plain C: integers, pointers, sizes.  No exceptions,
  * no C++ or torch types cross it.  Errors are errno values, as in opencrypto.
  * One espgpu_ctx per lcore thread (thread-compatible, not thread-safe), the
@@ -39,6 +40,8 @@ extern "C" {
 #define ESPGPU_CSP_F_ESN            0x0004   /* cryptodev.h:371 */
 #define ESPGPU_CRYPTO_SHA1_HMAC     7        /* cryptodev.h:150 */
 #define ESPGPU_CRYPTO_AES_CBC       11       /* cryptodev.h:155 */
+#define ESPGPU_CRYPTO_SHA2_256_HMAC 18     /* cryptodev.h:162 */
+#define ESPGPU_CRYPTO_AES_ICM       23       /* AES-CTR, cryptodev.h:167 */
 #define ESPGPU_CRYPTO_AES_NIST_GCM_16 25     /* cryptodev.h:169 */
 #define ESPGPU_CRYPTO_OP_DECRYPT    0x0      /* cryptodev.h:598 */
 #define ESPGPU_CRYPTO_OP_ENCRYPT    0x1
@@ -123,7 +126,7 @@ struct espgpu_desc {
 	uint16_t len;           /* ESP record length: SPI|SN|IV|payload|ICV          */
 	uint16_t sa;            /* session slot (espgpu_newsession's id)             */
 	uint32_t esn_hi;        /* high 32 bits of the ESN (SAs with CSP_F_ESN/SEP)  */
-	uint32_t salt;          /* GCM nonce salt = crp_iv[0..3] as stored in memory */
+	uint32_t salt;          /* GCM salt / AES-CTR nonce = crp_iv[0..3], in memory order */
 };
 
 struct espgpu_config {

@@ -25,20 +25,38 @@ class GcmSA:
         self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
         self.esn = esn
         self.mlen = mlen                # ICV bytes: 16, or 12 / 8 truncated (RFC 4106 s3.3)
+        self.hlen = 16
         self.oracle = O.SA(O.CSP_MODE_AEAD, self.key, self.salt, mlen=mlen,
                            flags=O.CSP_F_SEPARATE_AAD if esn else 0)
 
+    def esp_sa(self):
+        from espgpu.esp import GCM, SecAssoc
+        return SecAssoc(self.spi, GCM, self.key + self.salt, esn=self.esn, mlen=self.mlen)
+
 
 class EtaSA:
-    def __init__(self, rng, klen=32, esn=False, spi=None):
+    """An encrypt-then-MAC SA: AES-CBC (hlen 24) or AES-CTR (RFC 3686, hlen 16,
+    salt = the nonce) with HMAC-SHA1-96 or HMAC-SHA2-256-128."""
+
+    def __init__(self, rng, klen=32, esn=False, spi=None, ctr=False, sha256=False):
         self.key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
-        self.akey = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
-        self.salt = b"\0\0\0\0"
+        self.akey = rng.integers(0, 256, 32 if sha256 else 20, dtype=np.uint8).tobytes()
+        self.ctr, self.sha256 = ctr, sha256
+        self.salt = rng.integers(0, 256, 4, dtype=np.uint8).tobytes() if ctr else b"\0\0\0\0"
         self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
         self.esn = esn
-        self.mlen = 12                  # HMAC-SHA1-96
-        self.oracle = O.SA(O.CSP_MODE_ETA, self.key, akey=self.akey, mlen=12,
+        self.mlen = 16 if sha256 else 12    # HMAC-SHA2-256-128 / HMAC-SHA1-96
+        self.hlen = 16 if ctr else 24
+        self.oracle = O.SA(O.CSP_MODE_ETA, self.key, self.salt, akey=self.akey, mlen=self.mlen,
+                           calg=O.CRYPTO_AES_ICM if ctr else O.CRYPTO_AES_CBC,
+                           aalg=O.CRYPTO_SHA2_256_HMAC if sha256 else O.CRYPTO_SHA1_HMAC,
                            flags=O.CSP_F_ESN if esn else 0)
+
+    def esp_sa(self):
+        from espgpu.esp import CBC_SHA1, CBC_SHA256, CTR_SHA1, CTR_SHA256, SecAssoc
+        alg = {(0, 0): CBC_SHA1, (0, 1): CBC_SHA256, (1, 0): CTR_SHA1, (1, 1): CTR_SHA256}
+        return SecAssoc(self.spi, alg[(int(self.ctr), int(self.sha256))],
+                        self.key + (self.salt if self.ctr else b""), self.akey, esn=self.esn)
 
 
 def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None, tails=None):
@@ -50,9 +68,9 @@ def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None
     (last pad byte, pad length, next header).
     """
     n = len(sa_idx)
-    hlen = 16 if gcm else 24
     alens = np.array([sas[s].mlen for s in sa_idx], dtype=np.int64)
-    lens = np.array([hlen + int(c) + int(a) for c, a in zip(ct_lens, alens)], dtype=np.int64)
+    hlens = np.array([sas[s].hlen for s in sa_idx], dtype=np.int64)
+    lens = np.array([int(h) + int(c) + int(a) for h, c, a in zip(hlens, ct_lens, alens)], dtype=np.int64)
     offs = np.zeros(n, dtype=np.int64)
     pos = 0
     for i in range(n):

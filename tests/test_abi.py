@@ -45,6 +45,18 @@ def test_probesession_accepts_esp_gcm(klen):
                       csp_auth_mlen=mlen) == L.CRYPTODEV_PROBE_HARDWARE
 
 
+@pytest.mark.parametrize("calg", [L.CRYPTO_AES_CBC, L.CRYPTO_AES_ICM])
+@pytest.mark.parametrize("aalg,mlen", [(L.CRYPTO_SHA1_HMAC, 12), (L.CRYPTO_SHA2_256_HMAC, 16),
+                                       (L.CRYPTO_SHA2_256_HMAC, 0)])
+def test_probesession_accepts_eta_variants(calg, aalg, mlen):
+    """AES-CBC / AES-CTR (enc_xform ivsize 16, xform_aes_icm.c:69) with
+    HMAC-SHA1 or HMAC-SHA2-256 (esp_init, xform_esp.c:225-241)."""
+    for klen in (16, 24, 32):
+        assert _probe(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=calg, csp_cipher_klen=klen,
+                      csp_cipher_key=b"k" * klen, csp_auth_alg=aalg, csp_auth_klen=32,
+                      csp_auth_key=b"a" * 32, csp_auth_mlen=mlen) == L.CRYPTODEV_PROBE_HARDWARE
+
+
 def test_probesession_accepts_esp_cbc_sha1():
     assert _probe(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=L.CRYPTO_AES_CBC,
                   csp_cipher_klen=32, csp_cipher_key=b"k" * 32, csp_auth_alg=L.CRYPTO_SHA1_HMAC,
@@ -58,7 +70,13 @@ def test_probesession_accepts_esp_cbc_sha1():
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=25, csp_cipher_klen=16,
          csp_auth_alg=7, csp_auth_klen=20),                                                 # GCM as ETA
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
-         csp_auth_alg=9, csp_auth_klen=32),                                                 # SHA2 not served
+         csp_auth_alg=9, csp_auth_klen=32),                                                 # auth alg not served
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
+         csp_auth_alg=19, csp_auth_klen=48),                                                # SHA2-384 not served
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=12, csp_cipher_alg=23, csp_cipher_klen=16,
+         csp_auth_alg=7, csp_auth_klen=20),                                                 # CTR ivlen != 16
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=23, csp_cipher_klen=16,
+         csp_auth_alg=18, csp_auth_klen=32, csp_auth_mlen=36),                              # mlen > SHA-256
     dict(csp_mode=2, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16),                  # cipher-only
     dict(csp_mode=L.CSP_MODE_AEAD, csp_flags=0x1, csp_ivlen=12, csp_cipher_alg=25,
          csp_cipher_klen=16),                                                               # SEPARATE_OUTPUT

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import EtaSA, GcmSA, build_records, oracle_decrypt
+from helpers import EtaSA, GcmSA, build_records, golden, oracle_decrypt
 
 pytestmark = pytest.mark.gpu
 
@@ -31,14 +31,9 @@ def _descs_dev(descs):
 
 
 def _sessions(drv, sas):
-    from espgpu.esp import CBC_SHA1, GCM, SecAssoc
     sids = []
     for s in sas:
-        if isinstance(s, EtaSA):
-            sa = SecAssoc(s.spi, CBC_SHA1, s.key, s.akey, esn=s.esn)
-        else:
-            sa = SecAssoc(s.spi, GCM, s.key + s.salt, esn=s.esn)
-        rc, sid = drv.newsession(sa.csp())
+        rc, sid = drv.newsession(s.esp_sa().csp())
         assert rc == 0, drv.last_error()
         sids.append(sid)
     return sids
@@ -187,3 +182,198 @@ def test_eta_opencrypto_roundtrip(drv):
             fw.crypto_drain()
             assert c.crp_etype == O.EBADMSG
         fw.crypto_freesession(ses)
+
+
+# ---------------------------------------------------------------------------
+# AES-CTR (RFC 3686) and HMAC-SHA2-256 ETA sessions
+
+def _variant_sas(rng, esn=False):
+    return [EtaSA(rng, 16, esn=esn, ctr=c, sha256=h) for c in (False, True) for h in (False, True)] + \
+           [EtaSA(rng, 32, esn=esn, ctr=True, sha256=True), EtaSA(rng, 24, esn=esn, ctr=True)]
+
+
+def _variant_cts(rng, sas, sa_idx):
+    """CBC payloads are 16-byte multiples; CTR ones any 4-byte multiple."""
+    cbc = rng.choice([16, 32, 48, 208, 1440, 1456, 8944], len(sa_idx))
+    ctr = rng.choice([4, 8, 12, 20, 44, 100, 1444, 1448, 8948], len(sa_idx))
+    return np.where([sas[i].ctr for i in sa_idx], ctr, cbc)
+
+
+def _hl(sas, idx):
+    return np.array([sas[i].hlen for i in idx]), np.array([sas[i].mlen for i in idx])
+
+
+def _mask_var(descs, size, hl, ml):
+    m = np.zeros(size, dtype=bool)
+    for o4, L, h, a in zip(descs["off4"], descs["len"], hl, ml):
+        m[int(o4) * 4 + int(h):int(o4) * 4 + int(L) - int(a)] = True
+    return m
+
+
+@pytest.mark.parametrize("esn", [False, True])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace):
+    """AES-CBC / AES-CTR x HMAC-SHA1-96 / HMAC-SHA2-256-128 sessions mixed in
+    one batch (planner path), AES-128/192/256, tag failures anywhere in the
+    record: statuses and plaintext bit-exact vs the oracle, failed records
+    untouched in place."""
+    from espgpu.batch import decrypt_batch
+    rng = np.random.default_rng(1300 + 2 * esn + inplace)
+    sas = _variant_sas(rng, esn)
+    sids = _sessions(drv, sas)
+    n = 900
+    sa_idx = rng.integers(0, len(sas), n)
+    cts = _variant_cts(rng, sas, sa_idx)
+    eh = rng.integers(0, 2**32, n, dtype=np.uint32)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, esn_hi=eh)
+    bad = ct.copy()
+    flip = rng.random(n) < 0.07
+    for i in np.nonzero(flip)[0]:
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        bad[o + int(rng.integers(0, L))] ^= 0x10
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    arena = _dev(bad)
+    out = arena if inplace else torch.zeros_like(arena)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out, grouped=False)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy()
+    assert (got == ref_st).all(), np.nonzero(got != ref_st)[0][:10]
+    hl, ml = _hl(sas, sa_idx)
+    ok = got == 0
+    m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
+    res = out.cpu().numpy()
+    assert (res[m_ok] == plain[m_ok]).all()
+    if inplace:
+        m_bad = _mask_var(descs[~ok], len(bad), np.zeros((~ok).sum()), np.zeros((~ok).sum()))
+        assert (res[m_bad] == bad[m_bad]).all()
+    for s in sids:
+        drv.freesession(s)
+
+
+def test_eta_variants_encrypt_vs_oracle(drv):
+    from espgpu.batch import encrypt_batch
+    rng = np.random.default_rng(1400)
+    sas = _variant_sas(rng, esn=True)
+    sids = _sessions(drv, sas)
+    n = 600
+    sa_idx = rng.integers(0, len(sas), n)
+    cts = _variant_cts(rng, sas, sa_idx)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts,
+                                         esn_hi=rng.integers(0, 2**32, n, dtype=np.uint32))
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    arena = _dev(plain)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, _descs_dev(d), n, st)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert (arena.cpu().numpy() == ct).all()
+    for s in sids:
+        drv.freesession(s)
+
+
+def test_eta_variants_trailer(drv):
+    """The fused esp_input_cb trailer word for CTR records (partial last
+    block) and SHA2-256 sessions, out of place and in place."""
+    from espgpu.batch import decrypt_batch
+    from espgpu.esp import trailer_word
+    rng = np.random.default_rng(1500)
+    sas = _variant_sas(rng)
+    sids = _sessions(drv, sas)
+    n = 400
+    sa_idx = rng.integers(0, len(sas), n)
+    cts = _variant_cts(rng, sas, sa_idx)
+    tails = {i: bytes([int(rng.integers(0, 4)), int(rng.integers(0, 40)), int(rng.choice([4, 41, 59]))])
+             for i in range(n)}
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, tails=tails)
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    hl, ml = _hl(sas, sa_idx)
+    want = np.array([trailer_word(plain[int(o) * 4 + h:int(o) * 4 + int(L) - a])
+                     for o, L, h, a in zip(descs["off4"], descs["len"], hl, ml)], dtype=np.uint32)
+    for inplace in (False, True):
+        arena = _dev(ct)
+        out = arena if inplace else torch.zeros_like(arena)
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        trl = torch.zeros(n, dtype=torch.int32, device="cuda")
+        decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out, grouped=False, trailer=trl)
+        torch.cuda.synchronize()
+        assert (st.cpu().numpy() == 0).all()
+        assert (trl.cpu().numpy().view(np.uint32) == want).all(), inplace
+    for s in sids:
+        drv.freesession(s)
+
+
+@pytest.mark.parametrize("alg", ["ctr-sha1", "ctr-sha256", "cbc-sha256"])
+def test_eta_variants_opencrypto_roundtrip(drv, alg):
+    """esp_output -> esp_input through process/flush/poll for the AES-CTR
+    (crp_iv = nonce || IV || be32(1), xform_esp.c:453-458) and HMAC-SHA2-256
+    SAs: ciphertext and ICV bit-exact vs the oracle, flipped ICV -> EBADMSG."""
+    from espgpu.esp import CBC_SHA256, CTR_SHA1, CTR_SHA256, SecAssoc, esp_input_crp, esp_output_crp, esp_pad
+    from espgpu.opencrypto import CryptoFramework
+    fw = CryptoFramework(drv)
+    rng = np.random.default_rng(1600 + len(alg))
+    ctr, sha256 = alg.startswith("ctr"), alg.endswith("256")
+    name = {"ctr-sha1": CTR_SHA1, "ctr-sha256": CTR_SHA256, "cbc-sha256": CBC_SHA256}[alg]
+    ckey = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    nonce = rng.integers(0, 256, 4, dtype=np.uint8).tobytes() if ctr else b""
+    akey = rng.integers(0, 256, 32 if sha256 else 20, dtype=np.uint8).tobytes()
+    sa = SecAssoc(0x5150, name, ckey + nonce, akey)
+    err, ses = fw.crypto_newsession(sa.csp())
+    assert err == 0
+    orc = O.SA(O.CSP_MODE_ETA, ckey, nonce or b"\0\0\0\0", akey=akey, mlen=sa.mlen,
+               calg=O.CRYPTO_AES_ICM if ctr else O.CRYPTO_AES_CBC,
+               aalg=O.CRYPTO_SHA2_256_HMAC if sha256 else O.CRYPTO_SHA1_HMAC)
+    pkts, refs = [], []
+    for nbytes in (30, 61, 1400, 8900):
+        body = esp_pad(rng.integers(0, 256, nbytes, dtype=np.uint8).tobytes(), blocksize=4 if ctr else 16)
+        rec = (sa.spi.to_bytes(4, "big") + (3).to_bytes(4, "big") +
+               rng.integers(0, 256, sa.ivlen, dtype=np.uint8).tobytes() + body + bytes(sa.mlen))
+        e, ref = orc.esp_encrypt(rec)
+        assert e == 0
+        pkt = bytearray(bytes(20) + rec)
+        pkts.append(pkt)
+        refs.append((rec, ref))
+        assert fw.crypto_dispatch(esp_output_crp(fw, ses, sa, pkt, 20)) == 0
+    fw.crypto_drain()
+    for pkt, (rec, ref) in zip(pkts, refs):
+        assert bytes(pkt[20:]) == ref
+    crps = [esp_input_crp(fw, ses, sa, pkt, 20) for pkt in pkts]
+    bad = bytearray(pkts[2])
+    bad[-3] ^= 0x20
+    before = bytes(bad)
+    crps.append(esp_input_crp(fw, ses, sa, bad, 20))
+    for c in crps:
+        assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+    for c, pkt, (rec, ref) in zip(crps, pkts, refs):
+        assert c.crp_etype == 0
+        assert bytes(pkt[20 + sa.hlen:-sa.mlen]) == rec[sa.hlen:-sa.mlen]
+    assert crps[-1].crp_etype == O.EBADMSG and bytes(bad) == before
+    fw.crypto_freesession(ses)
+
+
+@pytest.mark.parametrize("v", golden("eta_esp_packets.json"), ids=lambda v: v["name"])
+def test_dpdk_cbc_sha256_esp_kat_opencrypto(drv, v):
+    """DPDK's AES-CBC + HMAC-SHA2-256-128 ESP tunnel packets decrypt through
+    the driver path to the expected inner packets."""
+    from espgpu.esp import CBC_SHA256, SecAssoc, esp_input_crp
+    from espgpu.opencrypto import CryptoFramework
+    fw = CryptoFramework(drv)
+    sa = SecAssoc(v["spi"], CBC_SHA256, bytes.fromhex(v["cipher_key"]), bytes.fromhex(v["auth_key"]))
+    assert sa.mlen == v["digest_len"]
+    err, ses = fw.crypto_newsession(sa.csp())
+    assert err == 0
+    skip = v["outer_hdr_len"]
+    pkt = bytearray(bytes(skip)) + bytearray(bytes.fromhex(v["esp_record"]))
+    c = esp_input_crp(fw, ses, sa, pkt, skip)
+    assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+    assert c.crp_etype == 0
+    inner = bytes.fromhex(v["inner_packet"])
+    assert bytes(pkt[skip + 24:skip + 24 + len(inner)]) == inner
+    fw.crypto_freesession(ses)
