@@ -127,6 +127,10 @@ def main():
                     help="time the verify-first in-place decrypt as the headline (default: out of place, "
                          "with the in-place rate reported beside it)")
     ap.add_argument("--no-inplace-leg", action="store_true", help="skip the in-place side measurement")
+    ap.add_argument("--tuning", action="append", default=[],
+                    help="experiment: espgpu_set_tuning key=value (e.g. grid=300; gcm_opts needs the knobs build)")
+    ap.add_argument("--nsa", type=int, default=0,
+                    help="experiment: override the config's SA count (0 = the config's own)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-to-host leg")
     ap.add_argument("--e2e-chunk", type=int, default=65536, help="records per pipelined step")
     args = ap.parse_args()
@@ -150,11 +154,17 @@ def main():
     from espgpu.esp import CBC_SHA1, GCM, SecAssoc
     from espgpu.opencrypto import GpuCryptoDriver
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.nsa:
+        cfg["nsa"] = args.nsa
+        cfg["workload"] += " [SA count overridden: %d]" % args.nsa
     rng = np.random.default_rng(0xE5B00001 + rank)
     spis, sa_of, sizes = plan_packets(cfg, rank, world, rng)
     n = len(sizes)
     drv = GpuCryptoDriver(device=local, max_sessions=max(16, len(spis) + 8))
+    for kv in args.tuning:
+        k, _, v = kv.partition("=")
+        assert drv.lib.espgpu_set_tuning(drv.ctx, k.encode(), int(v)) == 0, "tuning %s refused" % kv
     sids, salts, keys = [], [], []
     for spi in spis:
         if cfg["alg"] == "gcm":
@@ -207,7 +217,8 @@ def main():
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize()
-    assert int((status != 0).sum()) == 0, "decrypt/verify failed"
+    knobs = any(kv.startswith("gcm_opts=") and not kv.endswith("=0") for kv in args.tuning)
+    assert knobs or int((status != 0).sum()) == 0, "decrypt/verify failed"   # knobs break results on purpose
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -153,11 +153,12 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
   s3 = xor3(a3, b3, ror16(xor3(c3, d3, k.w)));
 }
 
-// Measurement knobs, compiled in only by `make KNOBS=1` (tools/gcm_timing.py
-// --opts): bit0 skips the record loads and plaintext stores, bit1 the GHASH
-// multiplies, bit2 the AES rounds after round 2, bit3 the stores only, bit4
-// the loads only.  They break results on
-// purpose, to split the kernel's time between memory, GHASH and AES.
+// Measurement knobs, compiled in only by `make knobs` (libespgpu_knobs.so;
+// tools/gcm_timing.py --opts, bench.py --tuning gcm_opts=N): bit0 skips the
+// record loads and plaintext stores, bit1 the GHASH multiplies, bit2 the AES
+// rounds after round 2, bit3 the stores only, bit4 the loads only, bit5 the
+// per-session GHASH table staging.  They break results on purpose, to split
+// the kernel's time between memory, GHASH, AES and per-session setup.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t g_opts;
 __device__ __forceinline__ uint32_t gopts() {
@@ -594,7 +595,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         flags = s->flags;
         mlen = s->mlen;
         mode = s->mode;
-        if (mode == ESPGPU_CSP_MODE_AEAD) {
+        if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
           const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + kGh8Off);
           uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
 #pragma unroll 4
