@@ -105,9 +105,14 @@ __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t 
     gcur[k] = roff;
     const uint32_t sa = k == 4 * nsas ? 0xffffffffu : (k >= eta0 ? k - eta0 : k % nsas);
     const uint32_t cls = k >= 4 * nsas ? 4u : 3u - k / nsas;
-    for (uint32_t j = 0; j * rpc < cnt; ++j, ++coff) {
-      if (coff < max_chunks)
-        chunks[coff] = Chunk{sa, roff + j * rpc, min(rpc, cnt - j * rpc), cls};
+    // ceil(cnt / rpc) chunks of EQUAL size (270 records -> 135 + 135, not
+    // 256 + 14): a workgroup's pass time grows with its busy waves, so a
+    // near-empty remainder chunk costs almost a full pass (cfg2: 1K sessions
+    // x 4 size classes leave ~256 +- 16 records per key)
+    const uint32_t nc = (cnt + rpc - 1) / rpc;
+    for (uint32_t j = 0; j < nc; ++j, ++coff) {
+      const uint32_t a = (uint32_t)((uint64_t)cnt * j / nc), b = (uint32_t)((uint64_t)cnt * (j + 1) / nc);
+      if (coff < max_chunks) chunks[coff] = Chunk{sa, roff + a, b - a, cls};
     }
     roff += cnt;
   }
