@@ -190,7 +190,12 @@ int  espgpu_get_stats(espgpu_ctx *ctx, struct espgpu_stats *st);
  * encrypt: payload encrypted in place, ICV written.
  * `flags`: ESPGPU_BATCH_GROUPED if d_desc is already grouped by session with
  * at most one session per run of 128 records (skips the device planner).
- * `stream` is a hipStream_t (NULL = default stream).  Asynchronous. */
+ * `stream` is a hipStream_t (NULL = default stream).  Asynchronous.
+ * Launches on one ctx are stream-ordered by the library: the work-queue
+ * counters and planner workspace belong to the ctx, so a launch on a stream
+ * other than the ctx's previous one first waits on an event recorded after
+ * that launch (never two kernels of one ctx at once).  Use one ctx per
+ * stream for concurrent batches. */
 #define ESPGPU_BATCH_GROUPED 0x1
 int  espgpu_decrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
                           uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t flags,

@@ -377,3 +377,47 @@ def test_dpdk_cbc_sha256_esp_kat_opencrypto(drv, v):
     inner = bytes.fromhex(v["inner_packet"])
     assert bytes(pkt[skip + 24:skip + 24 + len(inner)]) == inner
     fw.crypto_freesession(ses)
+
+
+def test_grouped_mode_mixed_run_fails_closed(drv):
+    """ESPGPU_BATCH_GROUPED trusts the caller's grouping only per record: in a
+    256-record GCM chunk led by an ETA record the GCM records come back
+    EINVAL (never an unauthenticated 0), GCM records of another session inside
+    a GCM-led chunk are EINVAL, and ETA records anywhere are still decrypted
+    and verified by the ETA kernel."""
+    from espgpu.batch import decrypt_batch
+    rng = np.random.default_rng(1700)
+    g1, g2, e1 = GcmSA(rng, 16), GcmSA(rng, 16), EtaSA(rng, 16)
+    sids = _sessions(drv, [g1, g2, e1])
+    # chunk 0 (records 0..255): ETA first, then GCM(g1); chunk 1: GCM(g1) first,
+    # then ETA and GCM(g2) records mixed in
+    n = 512
+    kinds = np.zeros(n, dtype=np.int64)          # 0 = g1, 1 = g2, 2 = e1
+    kinds[0] = 2
+    kinds[10:20] = 2
+    kinds[300:310] = 2
+    kinds[400:405] = 1
+    sas = [g1, g2, e1]
+    cts = np.where(kinds == 2, 1440, 1448)
+    plain, ct, descs, eh = build_records(rng, sas, kinds, cts)
+    d = descs.copy()
+    d["sa"] = [sids[k] for k in kinds]
+    ref_out, ref_st = oracle_decrypt(sas, ct, descs, eh)
+    assert (ref_st == 0).all()
+    arena, out = _dev(ct), torch.zeros(len(ct), dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    decrypt_batch(drv, arena, _descs_dev(d), n, st, out=out, grouped=True)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy()
+    eta = kinds == 2
+    assert (got[eta] == 0).all()                                 # ETA kernel owns them
+    assert (got[:256][kinds[:256] == 0] == O.EINVAL).all()       # ETA-led chunk: GCM fails closed
+    assert (got[256:][kinds[256:] == 0] == 0).all()              # its own session: decrypted
+    assert (got[kinds == 1] == O.EINVAL).all()                   # other GCM session in the chunk
+    res = out.cpu().numpy()
+    hl, ml = _hl(sas, kinds)
+    okm = got == 0
+    m = _mask_var(descs[okm], len(ct), hl[okm], ml[okm])
+    assert (res[m] == plain[m]).all()
+    for s in sids:
+        drv.freesession(s)
