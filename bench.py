@@ -128,7 +128,7 @@ def main():
                          "with the in-place rate reported beside it)")
     ap.add_argument("--no-inplace-leg", action="store_true", help="skip the in-place side measurement")
     ap.add_argument("--tuning", action="append", default=[],
-                    help="experiment: espgpu_set_tuning key=value (e.g. grid=300; gcm_opts needs the knobs build)")
+                    help="experiment: espgpu_set_tuning key=value (e.g. grid=300; gcm_opts and eta_opts need the knobs build)")
     ap.add_argument("--nsa", type=int, default=0,
                     help="experiment: override the config's SA count (0 = the config's own)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-to-host leg")
@@ -217,7 +217,7 @@ def main():
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize()
-    knobs = any(kv.startswith("gcm_opts=") and not kv.endswith("=0") for kv in args.tuning)
+    knobs = any(kv.split("=")[0] in ("gcm_opts", "eta_opts") and not kv.endswith("=0") for kv in args.tuning)
     assert knobs or int((status != 0).sum()) == 0, "decrypt/verify failed"   # knobs break results on purpose
     if world > 1:
         dist.barrier()

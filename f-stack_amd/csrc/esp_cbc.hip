@@ -56,6 +56,21 @@ constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
 
 typedef const __attribute__((address_space(4))) uint32_t *kptr;
 
+// Measurement knobs for the fused decrypt (MODE 0), compiled in only by
+// `make knobs` (bench.py --tuning eta_opts=N with ESPGPU_LIB pointing at
+// libespgpu_knobs.so): bit0 folds every record into the first 1 MiB of the
+// arena (L2-resident loads and stores), bit1 skips the AES rounds, bit2 the
+// HMAC compressions, bit3 the full chunks' plaintext stores.  They break
+// results on purpose, to split the kernel's time.
+#ifdef ESPGPU_KNOBS
+__device__ uint32_t e_opts;
+__device__ __forceinline__ uint32_t eopts() {
+  return *(const __attribute__((address_space(4))) uint32_t *)(const void *)&e_opts;
+}
+#else
+__device__ __forceinline__ constexpr uint32_t eopts() { return 0; }
+#endif
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
@@ -502,10 +517,10 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
         cy0 = m[14];
         cy1 = m[15];
         uint4 d[4] = {blk[0], blk[1], blk[2], blk[3]};
-        aes_dec4(d, key, nr, lds, slot);
+        if (!(eopts() & 2)) aes_dec4(d, key, nr, lds, slot);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if (k < nb) {
+          if (k < nb && !(eopts() & 8)) {
             st16(orec + HL + 16 * (i0 + k), xor4(d[k], prev));
             prev = blk[k];
           }
@@ -518,10 +533,10 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
         uint4 ks[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) ks[k] = make_uint4(salt, cy0, cy1, bswap32(4 * b + (uint32_t)k));
-        aes_enc4(ks, key, nr, te, slot);
+        if (!(eopts() & 2)) aes_enc4(ks, key, nr, te, slot);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if (b > 0 || k > 0)               // chunk 0 starts with SPI|SN|IV
+          if ((b > 0 || k > 0) && !(eopts() & 8))               // chunk 0 starts with SPI|SN|IV
             st16(orec + HL + 16 * (4 * b - 1 + (uint32_t)k),
                  xor4(make_uint4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]), ks[k]));
         }
@@ -588,7 +603,7 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
     uint32_t hn[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) hn[k] = h[k];
-    Hash<HS>::compress(hn, w);
+    if (!(eopts() & 4)) Hash<HS>::compress(hn, w);
     if (on) {
 #pragma unroll
       for (int k = 0; k < W; ++k) h[k] = hn[k];
@@ -754,8 +769,9 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         const DevSA *s = p.sas + sau;
         uint32_t trl = 0;
         const bool esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
+        const uint32_t roff = (eopts() & 1) ? (off & 0xffffcu) : off;
         const bool good = fused_hs<CKS == CK_CTR ? CK_CTR : CK_CBC>(
-            (int)s->aalg, p.arena + off, p.out + off, plen, s->mlen, esn, esnh, salt, kp(s->ipad), kp(s->opad),
+            (int)s->aalg, p.arena + roff, p.out + roff, plen, s->mlen, esn, esnh, salt, kp(s->ipad), kp(s->opad),
             kp(CKS == CK_CTR ? s->rk : s->dk), (int)s->nr, lds, slot, mine, &trl);
         if (mine) {
           ok = good;
@@ -847,6 +863,14 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 
 // 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
 // schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
+int set_eta_opts(uint32_t opts) {
+#ifdef ESPGPU_KNOBS
+  return hipMemcpyToSymbol(HIP_SYMBOL(e_opts), &opts, 4) == hipSuccess ? 0 : -1;
+#else
+  return opts ? -1 : 0;
+#endif
+}
+
 int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;

@@ -157,7 +157,7 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
 // tools/gcm_timing.py --opts, bench.py --tuning gcm_opts=N): bit0 skips the
 // record loads and plaintext stores, bit1 the GHASH multiplies, bit2 the AES
 // rounds after round 2, bit3 the stores only, bit4 the loads only, bit5 the
-// per-session GHASH table staging.  They break results on purpose, to split
+// per-session GHASH table staging, bit6 the per-record final multiply.  They break results on purpose, to split
 // the kernel's time between memory, GHASH, AES and per-session setup.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t g_opts;
@@ -502,7 +502,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     }
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
-  uint4 Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+  uint4 Z = (gopts() & 64) ? Y
+                           : gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 ej0 = shfl4(EJ0, (lane & ~(S - 1)) | pad);

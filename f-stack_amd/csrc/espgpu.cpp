@@ -810,6 +810,7 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
   if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
+  if (!strcmp(key, "eta_opts")) return set_eta_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
   return ESPGPU_ENOENT;
 }
 

@@ -110,6 +110,7 @@ __host__ __device__ inline uint32_t esp_trailer_word(uint32_t wlast, uint32_t pl
 // Launchers (defined in the .hip files, called by espgpu.cpp).
 int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream);
 int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
+int set_eta_opts(uint32_t opts);
 // kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones
 int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,

@@ -150,10 +150,12 @@ int main(int argc, char **argv) {
            "\"GBps\": %.1f}\n",                                                                           \
            g_block, SS, kn[KK], UU, NN, inplace, ms, b / ms / 1e6);                                       \
   }
-    for (int blk : {1024, 512, 256}) {
+    for (int blk : {768}) {
       g_block = blk;
       ONE(4, 0, 2, 0) ONE(4, 0, 4, 0) ONE(4, 0, 8, 0) ONE(8, 0, 2, 0) ONE(8, 0, 4, 0) ONE(16, 0, 1, 0) ONE(16, 0, 2, 0)
       ONE(4, 2, 2, 0) ONE(4, 1, 2, 0)
+      ONE(1, 1, 4, 0) ONE(1, 0, 4, 0) ONE(1, 2, 4, 0)   // lane = record, 64 B per step (the ETA kernel's pattern)
+      ONE(1, 0, 4, 1) ONE(1, 0, 4, 2) ONE(1, 0, 4, 3) ONE(1, 0, 8, 0) ONE(2, 0, 4, 0) ONE(4, 0, 4, 2)
     }
   }
   CK(hipDeviceSynchronize());
