@@ -127,6 +127,7 @@ def main():
                     help="time the verify-first in-place decrypt as the headline (default: out of place, "
                          "with the in-place rate reported beside it)")
     ap.add_argument("--no-inplace-leg", action="store_true", help="skip the in-place side measurement")
+    ap.add_argument("--no-encrypt-leg", action="store_true", help="skip the encrypt-direction side measurement")
     ap.add_argument("--tuning", action="append", default=[],
                     help="experiment: espgpu_set_tuning key=value (e.g. grid=300; gcm_opts and eta_opts need the knobs build)")
     ap.add_argument("--nsa", type=int, default=0,
@@ -271,6 +272,9 @@ def main():
         result["inplace"] = inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes,
                                         algo_bytes, world, dist, launched_kernel(cfg, True))
 
+    if not args.inplace and not args.no_encrypt_leg:
+        result["encrypt"] = encrypt_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, world, dist, cfg)
+
     if not args.no_e2e:
         result["e2e_pcie"] = e2e_leg(drv, pristine if args.inplace else arena, desc, d, n, pkt_bytes,
                                      args, world, dist)
@@ -347,6 +351,37 @@ def inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, algo_by
             "achieved_algorithmic_GBps": round(algo_bytes / (ms * 1e-3) / 1e9, 1),
             "status_ok": ok, "timing": "median of %d launches, HIP events around the decrypt only" % reps,
             "kernel": kernel + " (verify-first, in place)"}
+
+
+def encrypt_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, world, dist, cfg):
+    """The esp_output direction on the same records (espgpu_encrypt_batch, in
+    place: payload encrypted, ICV written), beside the headline.  Encrypting
+    any bytes is valid work, so the launches run back to back on a copy of the
+    arena; HIP events around the encrypt launches only."""
+    import torch
+    from espgpu.batch import encrypt_batch
+    work = arena.clone()
+    reps = 5
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps + 1)]
+    with torch.cuda.stream(stream):
+        for e0, e1 in evs:
+            e0.record(stream)
+            encrypt_batch(drv, work, desc, n, status, grouped=grouped, stream=stream)
+            e1.record(stream)
+    torch.cuda.synchronize()
+    ok = int((status != 0).sum()) == 0
+    ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs[1:])[reps // 2]
+    del work
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64, device=arena.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        b = torch.tensor([float(pkt_bytes)], dtype=torch.float64, device=arena.device)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        ms, pkt_bytes = float(t.item()), float(b.item())
+    kernel = "gcm_kernel<1, 1024>" if cfg["alg"] == "gcm" else "eta_kernel<1, 768, -1>"
+    return {"value": round(pkt_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "kernel_ms": round(ms, 4),
+            "status_ok": ok, "timing": "median of %d launches, HIP events around the encrypt only" % reps,
+            "kernel": kernel + " (in place, ICV written)"}
 
 
 def e2e_leg(drv, arena, desc, d, n, pkt_bytes, args, world, dist):

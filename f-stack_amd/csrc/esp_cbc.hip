@@ -39,6 +39,7 @@
 #include <algorithm>
 
 #include "espgpu_internal.h"
+#include "sha512_consts.h"
 
 namespace espgpu {
 
@@ -451,6 +452,112 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
   for (int k = 0; k < 8; ++k) out[k] = h[k];
 }
 
+// ---- SHA-512 / SHA-384 compression (SHA512_Transform, freebsd/crypto/sha2/sha512c.c:196) ----
+// 64-bit words held as uint64_t; rotations as two v_alignbit on the halves.
+__constant__ uint64_t kK512[80] = ESPGPU_SHA512_K;
+
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rl, rh;
+  if (n < 32) {
+    rl = __builtin_amdgcn_alignbit(hi, lo, n);
+    rh = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rl = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rh = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rh << 32) | rl;
+}
+
+__device__ __forceinline__ void sha512_compress(uint64_t h[8], uint64_t w[16]) {
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 80; ++t) {
+    uint64_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint64_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
+      const uint64_t s0 = rotr64(x, 1) ^ rotr64(x, 8) ^ (x >> 7);
+      const uint64_t s1 = rotr64(y, 19) ^ rotr64(y, 61) ^ (y >> 6);
+      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t t1 = hh + S1 + ch + kK512[t] + wt;
+    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    hh = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// 32-bit message word k (0..31) of the padded 128-byte block b of the inner
+// message rec[0, L0) || (esn ? be32(esn_hi) : ""); the 128-bit length field
+// is words 28..31 of the last block (its high 64 bits are zero)
+__device__ __forceinline__ uint32_t tail_word128(const uint8_t *rec, uint32_t b, int k, uint32_t L0, uint32_t L,
+                                                 bool esn, uint32_t esn_hi, uint32_t total, uint64_t bits) {
+  const uint32_t o = 128 * b + 4 * k;
+  uint32_t v;
+  if (o + 4 <= L0) v = bswap32(*reinterpret_cast<const uint32_t *>(rec + o));
+  else if (esn && o == L0) v = esn_hi;
+  else if (o == L) v = 0x80000000u;
+  else v = 0;
+  if (b == total - 1 && k == 30) v = (uint32_t)(bits >> 32);
+  if (b == total - 1 && k == 31) v = (uint32_t)bits;
+  return v;
+}
+
+// HMAC-SHA2-384 / -512 (hmac_init_pad states from the host: 16 words each,
+// word 2k = high half of state word k) of msg = rec[0, L0) || (esn ? be32(esn_hi) : "");
+// out = the 48- or 64-byte digest as big-endian 32-bit words
+__device__ void hmac_wide(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi, bool is384, kptr ipad,
+                          kptr opad, uint32_t out[16]) {
+  const uint32_t L = L0 + (esn ? 4u : 0u);
+  const uint32_t nfull = L0 / 128;                      // blocks entirely from memory
+  const uint32_t total = (L + 17 + 127) / 128;          // inner blocks incl. padding
+  const uint64_t bits = (uint64_t)(128 + L) * 8;        // the ipad block counts
+  const int dw = is384 ? 6 : 8;                         // digest words (64-bit)
+  uint64_t h[8], w[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = ((uint64_t)ipad[2 * k] << 32) | ipad[2 * k + 1];
+  for (uint32_t b = 0; b <= total; ++b) {
+    if (b < nfull) {
+      const uint8_t *p = rec + 128 * b;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 v = ld16(p + 16 * q);
+        w[2 * q] = ((uint64_t)bswap32(v.x) << 32) | bswap32(v.y);
+        w[2 * q + 1] = ((uint64_t)bswap32(v.z) << 32) | bswap32(v.w);
+      }
+    } else if (b < total) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        w[k] = ((uint64_t)tail_word128(rec, b, 2 * k, L0, L, esn, esn_hi, total, bits) << 32) |
+               tail_word128(rec, b, 2 * k + 1, L0, L, esn, esn_hi, total, bits);
+    } else {
+      // outer block: inner digest || 0x80 || 0... || bit length of (128 + digest)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = k < dw ? h[k] : (k == dw ? 0x8000000000000000ull : 0ull);
+      w[15] = (uint64_t)(128 + 8 * dw) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = ((uint64_t)opad[2 * k] << 32) | opad[2 * k + 1];
+    }
+    sha512_compress(h, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    out[2 * k] = (uint32_t)(h[k] >> 32);
+    out[2 * k + 1] = (uint32_t)h[k];
+  }
+}
+
+__device__ __forceinline__ bool wide_hash(uint32_t aalg) {
+  return aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || aalg == ESPGPU_CRYPTO_SHA2_512_HMAC;
+}
+
 __device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
 
 // One pass over an ETA record for the out-of-place decrypt: the record is
@@ -628,9 +735,12 @@ __device__ __forceinline__ bool fused_hs(int aalg, const uint8_t *rec, uint8_t *
                                         act, trl);
 }
 
+// out: the digest as big-endian words (5 / 8 / 12 / 16 of them)
 __device__ __forceinline__ void hmac_any(int aalg, const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi,
-                                         kptr ipad, kptr opad, uint32_t out[8]) {
-  if (aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+                                         kptr ipad, kptr opad, uint32_t out[16]) {
+  if (wide_hash((uint32_t)aalg))
+    hmac_wide(rec, L0, esn, esn_hi, aalg == ESPGPU_CRYPTO_SHA2_384_HMAC, ipad, opad, out);
+  else if (aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
     hmac_t<HS_SHA256>(rec, L0, esn, esn_hi, ipad, opad, out);
   else
     hmac_t<HS_SHA1>(rec, L0, esn, esn_hi, ipad, opad, out);
@@ -645,7 +755,11 @@ __device__ __forceinline__ void fill_pair(uint8_t *lds, uint32_t base, const uin
   }
 }
 
-// MODE 0: decrypt out-of-place; 1: encrypt in place; 2: decrypt in place (verify first)
+// MODE 0: decrypt out-of-place (fused, SHA-1 / SHA2-256 sessions of one cipher);
+// 1: encrypt in place; 2: decrypt in place (verify first); 3: decrypt out of
+// place for the SHA2-384/512 sessions (verify pass, then the block-parallel
+// pass of MODE 2 writing to p.out: 128-byte hash blocks do not line up with
+// MODE 0's four-block chunks)
 // CKS: MODE 0 is built once per cipher (CK_CBC / CK_CTR) and each launch
 // serves only its cipher's sessions -- both fused paths inlined in one kernel
 // made the register allocator spill; -1 = every ETA session.
@@ -702,8 +816,10 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           p.status[di] = ESPGPU_EINVAL;
           if (MODE != 1 && p.trailer) p.trailer[di] = 0;
         }
-      } else if (CKS >= 0 && (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR)) {
-        have = false;                                       // the other cipher's launch
+      } else if (MODE == 0 && ((s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR) || wide_hash(s->aalg))) {
+        have = false;                                       // another decrypt launch's session
+      } else if (MODE == 3 && !wide_hash(s->aalg)) {
+        have = false;                                       // the fused launches' session
       } else {
         const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;
         const uint32_t mlen = s->mlen;
@@ -713,8 +829,8 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         // blocksize (16 for CBC, 1 for CTR; records are 4-byte multiples)
         valid = pl > 0 && (ctr || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
-        if (valid && MODE == 2) {
-          uint32_t dg[8];
+        if (valid && (MODE == 2 || MODE == 3)) {
+          uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
           hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
                    kp(s->opad), dg);
@@ -747,7 +863,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
             prev = c;
           }
         }
-        uint32_t dg[8];
+        uint32_t dg[16];
         hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
                  kp(s->opad), dg);
         for (uint32_t k = 0; k < s->mlen / 4; ++k)
@@ -831,7 +947,8 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         const uint32_t rpl = __shfl(plen, j), rdi = __shfl(di, j), rsalt = __shfl(salt, j);
         if (f >= 0) {
           const uint32_t i = (uint32_t)f - sj;
-          uint8_t *rec = p.arena + ro;
+          const uint8_t *rec = p.arena + ro;
+          uint8_t *dst = (MODE == 3 ? p.out : p.arena) + ro;   // MODE 3: out of place
           const int rem = (int)rpl - 16 * (int)i;
           uint4 pt;
           if (ctr) {
@@ -839,12 +956,12 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
             const uint4 cb = make_uint4(rsalt, *reinterpret_cast<const uint32_t *>(rec + 8),
                                         *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(i + 1));
             pt = xor4(c, aes_enc(cb, kp(s->rk), nr, lds + LDS_TE, slot));
-            st_partial(rec + 16 + 16 * i, pt, rem);
+            st_partial(dst + 16 + 16 * i, pt, rem);
           } else {
             const uint4 c = ld16(rec + 24 + 16 * i);
             const uint4 prev = ld16(rec + 8 + 16 * i);       // C_{i-1}, or the IV for i = 0
             pt = xor4(aes_dec(c, kp(s->dk), nr, lds, slot), prev);
-            st16(rec + 24 + 16 * i, pt);
+            st16(dst + 24 + 16 * i, pt);
           }
           if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdi] = esp_trailer_word(last_word(pt, rem), rpl);
         }
@@ -861,8 +978,6 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 
 }  // namespace
 
-// 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
-// schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
 int set_eta_opts(uint32_t opts) {
 #ifdef ESPGPU_KNOBS
   return hipMemcpyToSymbol(HIP_SYMBOL(e_opts), &opts, 4) == hipSuccess ? 0 : -1;
@@ -871,6 +986,8 @@ int set_eta_opts(uint32_t opts) {
 #endif
 }
 
+// 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
+// schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
 int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
@@ -885,9 +1002,11 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *strea
   } else if (two_pass) {
     hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(grid), dim3(768), 0, st, p);
   } else {
-    // kinds: bit 0 = CBC sessions exist, bit 1 = CTR sessions exist
+    // kinds: bit 0 = SHA-1 / SHA2-256 CBC sessions exist, bit 1 = such CTR
+    // sessions, bit 2 = SHA2-384/512 sessions (either cipher)
     if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(grid), dim3(768), 0, st, p);
     if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(grid), dim3(768), 0, st, p);
+    if (kinds & 4) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(grid), dim3(768), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -34,6 +34,7 @@ struct Session {
   bool used = false;
   int mode = 0, flags = 0, mlen = 0, klen = 0;
   bool ctr = false;       // ETA with AES-ICM (RFC 3686 ESP AES-CTR)
+  bool wide = false;      // ETA with HMAC-SHA2-384/512 (128-byte hash blocks)
 };
 
 struct Pending {
@@ -94,7 +95,9 @@ struct espgpu_ctx {
   uint32_t *d_queue = nullptr;   // work queues: [0..1] GCM, [2..3] ETA (ticket, retired; self-resetting)
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
-  int n_eta = 0, n_ctr = 0;   // ETA sessions, of which AES-CTR
+  // ETA sessions: all, and by decrypt kernel: narrow-hash (SHA-1 / SHA2-256)
+  // CBC, narrow-hash CTR, wide-hash (SHA2-384/512, either cipher)
+  int n_eta = 0, n_cbc = 0, n_ctr = 0, n_wide = 0;
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -265,7 +268,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.isbox = c->d_isbox;
     q.status = d_status;
     q.nsas = nsas;
-    const int ek = (c->n_eta - c->n_ctr > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0);
+    const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wide > 0 ? 4 : 0);
     if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
@@ -396,8 +399,13 @@ int espgpu_probesession(const espgpu_session_params *csp) {
           !aes_klen)
         return ESPGPU_EINVAL;
       if (csp->csp_ivlen != 16) return ESPGPU_EINVAL;
-      const int hashlen = csp->csp_auth_alg == ESPGPU_CRYPTO_SHA1_HMAC ? 20
-                        : csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_256_HMAC ? 32 : 0;
+      int hashlen = 0;
+      switch (csp->csp_auth_alg) {                                 // xform_sha1.c, xform_sha2.c
+        case ESPGPU_CRYPTO_SHA1_HMAC: hashlen = 20; break;
+        case ESPGPU_CRYPTO_SHA2_256_HMAC: hashlen = 32; break;
+        case ESPGPU_CRYPTO_SHA2_384_HMAC: hashlen = 48; break;
+        case ESPGPU_CRYPTO_SHA2_512_HMAC: hashlen = 64; break;
+      }
       if (!hashlen || csp->csp_auth_klen <= 0) return ESPGPU_EINVAL;
       if (csp->csp_auth_mlen > hashlen || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
       if (csp->csp_flags & ESPGPU_CSP_F_SEPARATE_AAD) return ESPGPU_EINVAL;
@@ -442,17 +450,25 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     hc::ghash_tables(h, kGcmLanesPerRec, tabs.data());
     HIPCHK(c, hipMemcpy(c->d_gtab + (size_t)slot * kGhTableBytes, tabs.data(), kGhTableBytes, hipMemcpyHostToDevice));
   } else {
-    const bool sha256 = csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_256_HMAC;
+    const int aalg = csp->csp_auth_alg;
+    const bool sha256 = aalg == ESPGPU_CRYPTO_SHA2_256_HMAC;
+    const bool wide = aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || aalg == ESPGPU_CRYPTO_SHA2_512_HMAC;
     sa.calg = (uint32_t)csp->csp_cipher_alg;
-    sa.aalg = (uint32_t)csp->csp_auth_alg;
+    sa.aalg = (uint32_t)aalg;
     // mlen 0 = the whole hash (swcr_setup_auth, cryptosoft.c:1013-1018)
-    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : (sha256 ? 32u : 20u);
+    const uint32_t hashlen = sha256 ? 32u : aalg == ESPGPU_CRYPTO_SHA2_384_HMAC ? 48u
+                           : aalg == ESPGPU_CRYPTO_SHA2_512_HMAC ? 64u : 20u;
+    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : hashlen;
     for (int i = 0; i < 4 * (nr + 1); ++i) sa.rk[i] = rk[i];
     uint32_t dk[60];
     hc::aes_expand_dec(key, csp->csp_cipher_klen, dk);
     for (int i = 0; i < 4 * (nr + 1); ++i) sa.dk[i] = dk[i];
     const uint8_t *ak = (const uint8_t *)csp->csp_auth_key;
-    if (sha256) {
+    if (wide) {
+      const bool is384 = aalg == ESPGPU_CRYPTO_SHA2_384_HMAC;
+      hc::hmac_sha512_pad_state(ak, csp->csp_auth_klen, 0x36, is384, sa.ipad);
+      hc::hmac_sha512_pad_state(ak, csp->csp_auth_klen, 0x5c, is384, sa.opad);
+    } else if (sha256) {
       hc::hmac_sha256_pad_state(ak, csp->csp_auth_klen, 0x36, sa.ipad);
       hc::hmac_sha256_pad_state(ak, csp->csp_auth_klen, 0x5c, sa.opad);
     } else {
@@ -460,7 +476,9 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
       hc::hmac_sha1_pad_state(ak, csp->csp_auth_klen, 0x5c, sa.opad);
     }
     c->n_eta++;
-    if (csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM) c->n_ctr++;
+    if (wide) c->n_wide++;
+    else if (csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM) c->n_ctr++;
+    else c->n_cbc++;
   }
   HIPCHK(c, hipMemcpy(c->d_sas + slot, &sa, sizeof sa, hipMemcpyHostToDevice));
   Session &s = c->sessions[slot];
@@ -470,6 +488,8 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   s.mlen = (int)sa.mlen;
   s.klen = csp->csp_cipher_klen;
   s.ctr = csp->csp_mode == ESPGPU_CSP_MODE_ETA && csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
+  s.wide = csp->csp_mode == ESPGPU_CSP_MODE_ETA &&
+           (csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_384_HMAC || csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_512_HMAC);
   c->h_sas[slot] = sa;
   *sid_out = slot;
   return 0;
@@ -483,8 +503,13 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
   for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
-  if (c->sessions[sid].mode == ESPGPU_CSP_MODE_ETA) c->n_eta--;
-  if (c->sessions[sid].ctr) c->n_ctr--;
+  const Session &fs = c->sessions[sid];
+  if (fs.mode == ESPGPU_CSP_MODE_ETA) {
+    c->n_eta--;
+    if (fs.wide) c->n_wide--;
+    else if (fs.ctr) c->n_ctr--;
+    else c->n_cbc--;
+  }
   c->sessions[sid] = Session();
   DevSA z;
   memset(&z, 0, sizeof z);

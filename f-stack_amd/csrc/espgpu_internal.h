@@ -23,11 +23,12 @@ struct DevSA {
   uint32_t mode;    // ESPGPU_CSP_MODE_AEAD / _ETA, 0 = free slot
   uint32_t flags;   // csp_flags
   uint32_t mlen;    // ICV bytes compared / written
-  uint32_t ipad[8]; // ETA: HMAC chaining states after the ipad / opad key
-  uint32_t opad[8]; //      block (5 words SHA-1, 8 words SHA2-256)
+  uint32_t ipad[16]; // ETA: HMAC chaining states after the ipad / opad key
+  uint32_t opad[16]; //      block (5 words SHA-1, 8 SHA2-256, 16 SHA2-384/512:
+                     //      64-bit state word k as words 2k (high), 2k+1)
   uint32_t calg;    // ETA cipher: ESPGPU_CRYPTO_AES_CBC or _AES_ICM (CTR)
-  uint32_t aalg;    // ETA auth: ESPGPU_CRYPTO_SHA1_HMAC or _SHA2_256_HMAC
-  uint32_t pad_[256 - 128 - 4 - 16 - 2];
+  uint32_t aalg;    // ETA auth: ESPGPU_CRYPTO_SHA1_HMAC or _SHA2_256/384/512_HMAC
+  uint32_t pad_[256 - 128 - 4 - 32 - 2];
 };
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 

@@ -1,5 +1,6 @@
 // host_crypto.cpp — see host_crypto.h.
 #include "host_crypto.h"
+#include "sha512_consts.h"
 
 #include <string.h>
 
@@ -298,6 +299,70 @@ void hmac_sha256_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_
   for (int i = 0; i < 64; ++i) k[i] ^= padval;
   memcpy(h, kSha256Iv, 32);
   sha256_compress(h, k);
+}
+
+// SHA-512 / SHA-384 (FIPS 180-4; freebsd/crypto/sha2/sha512c.c SHA512_Transform
+// :196): 128-byte blocks of 64-bit words; constants from sha512_consts.h
+static const uint64_t K512[80] = ESPGPU_SHA512_K;
+static const uint64_t kSha512Iv[8] = ESPGPU_SHA512_IV, kSha384Iv[8] = ESPGPU_SHA384_IV;
+static inline uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+static inline uint64_t be64(const uint8_t *p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+
+void sha512_compress(uint64_t h[8], const uint8_t blk[128]) {
+  uint64_t w[80], v[8];
+  for (int i = 0; i < 16; ++i) w[i] = be64(blk + 8 * i);
+  for (int i = 16; i < 80; ++i) {
+    const uint64_t s0 = rotr64(w[i - 15], 1) ^ rotr64(w[i - 15], 8) ^ (w[i - 15] >> 7);
+    const uint64_t s1 = rotr64(w[i - 2], 19) ^ rotr64(w[i - 2], 61) ^ (w[i - 2] >> 6);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  for (int i = 0; i < 8; ++i) v[i] = h[i];
+  for (int i = 0; i < 80; ++i) {
+    const uint64_t t1 = v[7] + (rotr64(v[4], 14) ^ rotr64(v[4], 18) ^ rotr64(v[4], 41)) +
+                        ((v[4] & v[5]) ^ (~v[4] & v[6])) + K512[i] + w[i];
+    const uint64_t t2 = (rotr64(v[0], 28) ^ rotr64(v[0], 34) ^ rotr64(v[0], 39)) +
+                        ((v[0] & v[1]) ^ (v[0] & v[2]) ^ (v[1] & v[2]));
+    v[7] = v[6]; v[6] = v[5]; v[5] = v[4]; v[4] = v[3] + t1;
+    v[3] = v[2]; v[2] = v[1]; v[1] = v[0]; v[0] = t1 + t2;
+  }
+  for (int i = 0; i < 8; ++i) h[i] += v[i];
+}
+
+static void sha512_full(const uint8_t *m, int len, bool is384, uint8_t out[64]) {
+  uint64_t h[8];
+  memcpy(h, is384 ? kSha384Iv : kSha512Iv, sizeof h);
+  int off = 0;
+  for (; len - off >= 128; off += 128) sha512_compress(h, m + off);
+  uint8_t tail[256] = {0};
+  const int rem = len - off;
+  memcpy(tail, m + off, (size_t)rem);
+  tail[rem] = 0x80;
+  const int tl = (rem + 17 <= 128) ? 128 : 256;
+  const uint64_t bits = (uint64_t)len * 8;          // the high 64 bits of the 128-bit length are 0
+  for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+  sha512_compress(h, tail);
+  if (tl == 256) sha512_compress(h, tail + 128);
+  for (int i = 0; i < (is384 ? 6 : 8); ++i) {
+    put_be32(out + 8 * i, (uint32_t)(h[i] >> 32));
+    put_be32(out + 8 * i + 4, (uint32_t)h[i]);
+  }
+}
+
+// hmac_init_pad (crypto.c:413-441) for HMAC-SHA2-384/512: the state after the
+// key padded to 128 bytes (hashed first when longer), as 16 words: word 2k is
+// the high half of state word k, 2k+1 the low half
+void hmac_sha512_pad_state(const uint8_t *key, int klen, uint8_t padval, bool is384, uint32_t out[16]) {
+  uint8_t k[128] = {0};
+  if (klen > 128) sha512_full(key, klen, is384, k);
+  else if (klen > 0) memcpy(k, key, (size_t)klen);
+  for (int i = 0; i < 128; ++i) k[i] ^= padval;
+  uint64_t h[8];
+  memcpy(h, is384 ? kSha384Iv : kSha512Iv, sizeof h);
+  sha512_compress(h, k);
+  for (int i = 0; i < 8; ++i) {
+    out[2 * i] = (uint32_t)(h[i] >> 32);
+    out[2 * i + 1] = (uint32_t)h[i];
+  }
 }
 
 }  // namespace hc

@@ -35,6 +35,8 @@ void sha1_compress(uint32_t h[5], const uint8_t block[64]);
 void hmac_sha1_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t h[5]);
 void sha256_compress(uint32_t h[8], const uint8_t block[64]);
 void hmac_sha256_pad_state(const uint8_t *key, int klen, uint8_t padval, uint32_t h[8]);
+void sha512_compress(uint64_t h[8], const uint8_t block[128]);
+void hmac_sha512_pad_state(const uint8_t *key, int klen, uint8_t padval, bool is384, uint32_t h[16]);
 
 }  // namespace hc
 }  // namespace espgpu

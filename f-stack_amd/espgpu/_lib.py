@@ -19,6 +19,8 @@ CSP_F_ESN = 0x4
 CRYPTO_SHA1_HMAC = 7
 CRYPTO_AES_CBC = 11
 CRYPTO_SHA2_256_HMAC = 18
+CRYPTO_SHA2_384_HMAC = 19
+CRYPTO_SHA2_512_HMAC = 20
 CRYPTO_AES_ICM = 23
 CRYPTO_AES_NIST_GCM_16 = 25
 CRYPTO_OP_DECRYPT = 0x0

@@ -13,9 +13,18 @@ from . import _lib as L
 from .opencrypto import crypto_session_params
 
 GCM, CBC_SHA1 = "aes-gcm-16", "aes-cbc-hmac-sha1-96"
-CBC_SHA256 = "aes-cbc-hmac-sha2-256-128"
+CBC_SHA256, CBC_SHA384, CBC_SHA512 = ("aes-cbc-hmac-sha2-256-128", "aes-cbc-hmac-sha2-384-192",
+                                      "aes-cbc-hmac-sha2-512-256")
 CTR_SHA1, CTR_SHA256 = "aes-ctr-hmac-sha1-96", "aes-ctr-hmac-sha2-256-128"   # RFC 3686
-ETA_ALGS = (CBC_SHA1, CBC_SHA256, CTR_SHA1, CTR_SHA256)
+CTR_SHA384, CTR_SHA512 = "aes-ctr-hmac-sha2-384-192", "aes-ctr-hmac-sha2-512-256"
+# auth algorithm and ICV bytes (xform_ah_authsize, xform_ah.c:117-131: 12 for
+# SHA1-96, hashsize/2 for SHA2 per RFC 4868)
+_AUTH = {CBC_SHA1: (L.CRYPTO_SHA1_HMAC, 12), CTR_SHA1: (L.CRYPTO_SHA1_HMAC, 12),
+         CBC_SHA256: (L.CRYPTO_SHA2_256_HMAC, 16), CTR_SHA256: (L.CRYPTO_SHA2_256_HMAC, 16),
+         CBC_SHA384: (L.CRYPTO_SHA2_384_HMAC, 24), CTR_SHA384: (L.CRYPTO_SHA2_384_HMAC, 24),
+         CBC_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32), CTR_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32)}
+_CTR_ALGS = (CTR_SHA1, CTR_SHA256, CTR_SHA384, CTR_SHA512)
+ETA_ALGS = tuple(_AUTH)
 IPPROTO_NONE = 59
 
 
@@ -28,14 +37,14 @@ class SecAssoc:
         self.key = bytes(key)          # GCM: cipher key || 4-byte salt (RFC 4106 8.1)
         self.auth_key = bytes(auth_key)
         self.esn = esn
-        # ICV bytes: xform_ah_authsize (GMAC 16, SHA1-HMAC 12, SHA2-256-HMAC
-        # 16 = hashsize/2); a GCM SA may carry a truncated 12- or 8-byte ICV
+        # ICV bytes: xform_ah_authsize (GMAC 16, SHA1-HMAC 12, SHA2-HMAC
+        # hashsize/2); a GCM SA may carry a truncated 12- or 8-byte ICV
         # (RFC 4106 s3.3, csp_auth_mlen)
-        self.mlen = mlen if mlen is not None else (12 if alg in (CBC_SHA1, CTR_SHA1) else 16)
+        self.mlen = mlen if mlen is not None else (16 if alg == GCM else _AUTH[alg][1])
 
     @property
     def ctr(self):
-        return self.alg in (CTR_SHA1, CTR_SHA256)
+        return self.alg in _CTR_ALGS
 
     @property
     def cipher_alg(self):
@@ -43,7 +52,7 @@ class SecAssoc:
 
     @property
     def auth_alg(self):
-        return L.CRYPTO_SHA2_256_HMAC if self.alg in (CBC_SHA256, CTR_SHA256) else L.CRYPTO_SHA1_HMAC
+        return _AUTH[self.alg][0]
 
     @property
     def ivlen(self):
@@ -59,7 +68,7 @@ class SecAssoc:
 
     @property
     def blocksize(self):
-        return 16 if self.alg in (CBC_SHA1, CBC_SHA256) else 1   # enc_xform blocksize (ESP pads to 4 anyway)
+        return 1 if self.alg == GCM or self.ctr else 16    # enc_xform blocksize (ESP pads to 4 anyway)
 
     @property
     def salt(self):

@@ -7,7 +7,8 @@
  * (freebsd/opencrypto/cryptosoft.c) for the ESP ciphers F-Stack's IPsec uses:
  *   AES-GCM-16 (CSP_MODE_AEAD)                  -> swcr_gcm      cryptosoft.c:465-645
  *   AES-CBC or AES-CTR (RFC 3686) + HMAC-SHA1-96
- *     or HMAC-SHA2-256-128 (CSP_MODE_ETA)       -> swcr_eta      cryptosoft.c:874-888
+ *     or HMAC-SHA2-256-128 / -384-192 / -512-256
+ *     (CSP_MODE_ETA)                            -> swcr_eta      cryptosoft.c:874-888
  * Every entry point is plain C: integers, pointers, sizes.  No exceptions,
  * no C++ or torch types cross it.  Errors are errno values, as in opencrypto.
  * One espgpu_ctx per lcore thread (thread-compatible, not thread-safe), the
@@ -41,6 +42,8 @@ extern "C" {
 #define ESPGPU_CRYPTO_SHA1_HMAC     7        /* cryptodev.h:150 */
 #define ESPGPU_CRYPTO_AES_CBC       11       /* cryptodev.h:155 */
 #define ESPGPU_CRYPTO_SHA2_256_HMAC 18     /* cryptodev.h:162 */
+#define ESPGPU_CRYPTO_SHA2_384_HMAC 19     /* cryptodev.h:163 */
+#define ESPGPU_CRYPTO_SHA2_512_HMAC 20     /* cryptodev.h:164 */
 #define ESPGPU_CRYPTO_AES_ICM       23       /* AES-CTR, cryptodev.h:167 */
 #define ESPGPU_CRYPTO_AES_NIST_GCM_16 25     /* cryptodev.h:169 */
 #define ESPGPU_CRYPTO_OP_DECRYPT    0x0      /* cryptodev.h:598 */

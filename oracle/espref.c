@@ -12,6 +12,7 @@
  * deliberately mirrors cryptosoft.c so that its timing is "cryptosoft-shaped".
  */
 #include "espref.h"
+#include "sha512_consts.h"
 
 #include <errno.h>
 #include <pthread.h>
@@ -633,27 +634,77 @@ static void sha256_block(uint32_t h[8], const uint8_t *m)
 		h[i] += v[i];
 }
 
-/* A hash context for either auth algorithm of an ETA session. */
+/* ------------------------------------------------------------------------ */
+/* SHA-512 / SHA-384 (freebsd/crypto/sha2/sha512c.c: K[] :152, SHA512_Transform */
+/* :196, SHA512_Init :440, SHA384_Init :493); 128-byte blocks, 64-bit words,  */
+/* a 128-bit length field.  Constants: sha512_consts.h (FIPS 180-4).          */
+
+static const uint64_t SHA512_K[80] = OREF_SHA512_K;
+
+static uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+static void sha512_block(uint64_t h[8], const uint8_t *m)
+{
+	uint64_t w[80], v[8];
+
+	for (int t = 0; t < 16; t++)
+		w[t] = ld_be64(m + 8 * t);
+	for (int t = 16; t < 80; t++) {
+		uint64_t s0 = ror64(w[t - 15], 1) ^ ror64(w[t - 15], 8) ^ (w[t - 15] >> 7);
+		uint64_t s1 = ror64(w[t - 2], 19) ^ ror64(w[t - 2], 61) ^ (w[t - 2] >> 6);
+		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+	}
+	memcpy(v, h, sizeof(v));
+	for (int t = 0; t < 80; t++) {
+		uint64_t S1 = ror64(v[4], 14) ^ ror64(v[4], 18) ^ ror64(v[4], 41);
+		uint64_t ch = (v[4] & v[5]) ^ (~v[4] & v[6]);
+		uint64_t t1 = v[7] + S1 + ch + SHA512_K[t] + w[t];
+		uint64_t S0 = ror64(v[0], 28) ^ ror64(v[0], 34) ^ ror64(v[0], 39);
+		uint64_t maj = (v[0] & v[1]) ^ (v[0] & v[2]) ^ (v[1] & v[2]);
+		v[7] = v[6]; v[6] = v[5]; v[5] = v[4]; v[4] = v[3] + t1;
+		v[3] = v[2]; v[2] = v[1]; v[1] = v[0]; v[0] = t1 + S0 + maj;
+	}
+	for (int i = 0; i < 8; i++)
+		h[i] += v[i];
+}
+
+/* A hash context for any auth algorithm of an ETA session. */
 struct hctx {
-	int alg;                /* OREF_CRYPTO_SHA1_HMAC or OREF_CRYPTO_SHA2_256_HMAC */
-	uint32_t h[8];
+	int alg;                /* OREF_CRYPTO_SHA1_HMAC, _SHA2_256/384/512_HMAC */
+	uint32_t h[8];          /* SHA-1 / SHA-256 state */
+	uint64_t h64[8];        /* SHA-384 / SHA-512 state */
 	uint64_t nbytes;
-	uint8_t buf[64];
+	uint8_t buf[128];
 	unsigned fill;
 };
 
-static int hash_len(int alg) { return alg == OREF_CRYPTO_SHA2_256_HMAC ? 32 : 20; }
+static int wide(int alg) { return alg == OREF_CRYPTO_SHA2_384_HMAC || alg == OREF_CRYPTO_SHA2_512_HMAC; }
+static int block_len(int alg) { return wide(alg) ? 128 : 64; }
+static int hash_len(int alg)
+{
+	switch (alg) {
+	case OREF_CRYPTO_SHA2_256_HMAC: return 32;
+	case OREF_CRYPTO_SHA2_384_HMAC: return 48;
+	case OREF_CRYPTO_SHA2_512_HMAC: return 64;
+	default: return 20;
+	}
+}
 
 static void h_init(struct hctx *c, int alg)
 {
 	static const uint32_t iv256[8] = { 0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
 	    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19 };
+	static const uint64_t iv512[8] = OREF_SHA512_IV, iv384[8] = OREF_SHA384_IV;
 	struct sha1_ctx s1;
 
 	memset(c, 0, sizeof(*c));
 	c->alg = alg;
 	if (alg == OREF_CRYPTO_SHA2_256_HMAC) {
 		memcpy(c->h, iv256, sizeof(iv256));
+	} else if (alg == OREF_CRYPTO_SHA2_384_HMAC) {
+		memcpy(c->h64, iv384, sizeof(iv384));
+	} else if (alg == OREF_CRYPTO_SHA2_512_HMAC) {
+		memcpy(c->h64, iv512, sizeof(iv512));
 	} else {
 		sha1_init(&s1);
 		memcpy(c->h, s1.h, sizeof(s1.h));
@@ -662,7 +713,9 @@ static void h_init(struct hctx *c, int alg)
 
 static void h_block(struct hctx *c, const uint8_t *m)
 {
-	if (c->alg == OREF_CRYPTO_SHA2_256_HMAC)
+	if (wide(c->alg))
+		sha512_block(c->h64, m);
+	else if (c->alg == OREF_CRYPTO_SHA2_256_HMAC)
 		sha256_block(c->h, m);
 	else
 		sha1_block(c->h, m);
@@ -670,34 +723,46 @@ static void h_block(struct hctx *c, const uint8_t *m)
 
 static void h_update(struct hctx *c, const uint8_t *p, size_t n)
 {
+	const unsigned bl = (unsigned)block_len(c->alg);
+
 	c->nbytes += n;
 	while (n > 0) {
-		size_t k = 64 - c->fill;
+		size_t k = bl - c->fill;
 		if (k > n)
 			k = n;
 		memcpy(c->buf + c->fill, p, k);
 		c->fill += (unsigned)k;
 		p += k;
 		n -= k;
-		if (c->fill == 64) {
+		if (c->fill == bl) {
 			h_block(c, c->buf);
 			c->fill = 0;
 		}
 	}
 }
 
+/* padding: 0x80, zeros, then the bit length in 8 (SHA-1/256) or 16 bytes */
 static void h_final(uint8_t *out, struct hctx *c)
 {
+	const unsigned bl = (unsigned)block_len(c->alg), lf = wide(c->alg) ? 16 : 8;
 	uint64_t bits = c->nbytes * 8;
-	uint8_t pad = 0x80, z = 0, lb[8];
+	uint8_t pad = 0x80, z = 0, lb[16];
 
 	h_update(c, &pad, 1);
-	while (c->fill != 56)
+	while (c->fill != bl - lf)
 		h_update(c, &z, 1);
-	st_be64(lb, bits);
-	h_update(c, lb, 8);
-	for (int i = 0; i < hash_len(c->alg) / 4; i++)
-		st_be32(out + 4 * i, c->h[i]);
+	memset(lb, 0, sizeof(lb));
+	st_be64(lb + lf - 8, bits);
+	h_update(c, lb, lf);
+	if (wide(c->alg)) {
+		for (int i = 0; i < hash_len(c->alg) / 8; i++) {
+			st_be32(out + 8 * i, (uint32_t)(c->h64[i] >> 32));
+			st_be32(out + 8 * i + 4, (uint32_t)c->h64[i]);
+		}
+	} else {
+		for (int i = 0; i < hash_len(c->alg) / 4; i++)
+			st_be32(out + 4 * i, c->h[i]);
+	}
 }
 
 void oref_sha256(const uint8_t *msg, size_t len, uint8_t out[32])
@@ -709,13 +774,15 @@ void oref_sha256(const uint8_t *msg, size_t len, uint8_t out[32])
 	h_final(out, &c);
 }
 
-/* hmac_init_pad (crypto.c:413-441) for either hash */
+/* hmac_init_pad (crypto.c:413-441) for any hash: the key padded to the
+ * hash's block (64 or 128 bytes), hashed first when longer */
 static void h_hmac_pad(const uint8_t *key, int klen, struct hctx *c, int alg, uint8_t padval)
 {
-	uint8_t k[64];
+	const int bl = block_len(alg);
+	uint8_t k[128];
 
 	memset(k, 0, sizeof(k));
-	if (klen > 64) {
+	if (klen > bl) {
 		struct hctx t;
 		h_init(&t, alg);
 		h_update(&t, key, (size_t)klen);
@@ -723,16 +790,25 @@ static void h_hmac_pad(const uint8_t *key, int klen, struct hctx *c, int alg, ui
 	} else {
 		memcpy(k, key, (size_t)klen);
 	}
-	for (int i = 0; i < 64; i++)
+	for (int i = 0; i < bl; i++)
 		k[i] ^= padval;
 	h_init(c, alg);
-	h_update(c, k, 64);
+	h_update(c, k, (size_t)bl);
+}
+
+void oref_hash(int alg, const uint8_t *msg, size_t len, uint8_t *out)
+{
+	struct hctx c;
+
+	h_init(&c, alg);
+	h_update(&c, msg, len);
+	h_final(out, &c);
 }
 
 void oref_hmac(int alg, const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t *out)
 {
 	struct hctx i, o;
-	uint8_t inner[32];
+	uint8_t inner[64];
 
 	h_hmac_pad(key, klen, &i, alg, 0x36);
 	h_hmac_pad(key, klen, &o, alg, 0x5c);
@@ -803,7 +879,8 @@ oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int ck
 			memcpy(sa->salt, salt, 4);
 	} else if (mode == OREF_CSP_MODE_ETA) {         /* swcr_setup_cipher/auth */
 		if ((calg != OREF_CRYPTO_AES_CBC && calg != OREF_CRYPTO_AES_ICM) ||
-		    (aalg != OREF_CRYPTO_SHA1_HMAC && aalg != OREF_CRYPTO_SHA2_256_HMAC)) {
+		    (aalg != OREF_CRYPTO_SHA1_HMAC && aalg != OREF_CRYPTO_SHA2_256_HMAC &&
+		     aalg != OREF_CRYPTO_SHA2_384_HMAC && aalg != OREF_CRYPTO_SHA2_512_HMAC)) {
 			free(sa);
 			return NULL;
 		}
@@ -953,11 +1030,11 @@ static int swcr_encdec_cbc(const oref_sa *sa, struct req *r)
 	return 0;
 }
 
-/* swcr_authcompute for HMAC-SHA1 / HMAC-SHA2-256 (cryptosoft.c:317-382) */
+/* swcr_authcompute for HMAC-SHA1 / HMAC-SHA2 (cryptosoft.c:317-382) */
 static int swcr_authcompute_c(const oref_sa *sa, struct req *r)
 {
 	struct hctx ctx;
-	uint8_t a[32];
+	uint8_t a[64];
 
 	memcpy(&ctx, &sa->ictx, sizeof(ctx));
 	h_update(&ctx, r->buf + r->aad_start, (size_t)r->aad_len);

@@ -39,6 +39,8 @@ extern "C" {
 #define OREF_CRYPTO_SHA1_HMAC      7
 #define OREF_CRYPTO_AES_CBC        11
 #define OREF_CRYPTO_SHA2_256_HMAC  18
+#define OREF_CRYPTO_SHA2_384_HMAC  19     /* cryptodev.h:163 */
+#define OREF_CRYPTO_SHA2_512_HMAC  20     /* cryptodev.h:164 */
 #define OREF_CRYPTO_AES_ICM        23          /* AES-CTR */
 #define OREF_CRYPTO_AES_NIST_GCM_16 25
 
@@ -54,7 +56,9 @@ void oref_gf128_mul(const uint8_t h[16], const uint8_t x[16], uint8_t out[16]);
 void oref_sha1(const uint8_t *msg, size_t len, uint8_t out[20]);
 void oref_hmac_sha1(const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t out[20]);
 void oref_sha256(const uint8_t *msg, size_t len, uint8_t out[32]);
-/* HMAC with alg = OREF_CRYPTO_SHA1_HMAC (20-byte out) or _SHA2_256_HMAC (32) */
+/* hash / HMAC with alg = OREF_CRYPTO_SHA1_HMAC (20-byte out), _SHA2_256_HMAC
+ * (32), _SHA2_384_HMAC (48) or _SHA2_512_HMAC (64) */
+void oref_hash(int alg, const uint8_t *msg, size_t len, uint8_t *out);
 void oref_hmac(int alg, const uint8_t *key, int klen, const uint8_t *msg, size_t len, uint8_t *out);
 /* AES-ICM (counter mode, full 128-bit big-endian increment) from ctr[16] */
 void oref_aes_ctr(const uint8_t *key, int klen, const uint8_t ctr[16], uint8_t *data, int len);
@@ -80,7 +84,7 @@ oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
                      const uint8_t salt[4], const uint8_t *akey, int aklen, int mlen);
 /* ETA with a chosen cipher (OREF_CRYPTO_AES_CBC, or _AES_ICM: RFC 3686 ESP
  * AES-CTR, salt = the 4-byte nonce esp_init strips from the key) and HMAC
- * (OREF_CRYPTO_SHA1_HMAC or _SHA2_256_HMAC; mlen 0 = the full hash). */
+ * (OREF_CRYPTO_SHA1_HMAC or _SHA2_256/384/512_HMAC; mlen 0 = the full hash). */
 oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int cklen,
                       const uint8_t salt[4], int aalg, const uint8_t *akey, int aklen, int mlen);
 void oref_sa_free(oref_sa *sa);

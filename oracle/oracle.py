@@ -17,6 +17,9 @@ CSP_MODE_ETA = 5
 CRYPTO_SHA1_HMAC = 7
 CRYPTO_AES_CBC = 11
 CRYPTO_SHA2_256_HMAC = 18
+CRYPTO_SHA2_384_HMAC = 19
+CRYPTO_SHA2_512_HMAC = 20
+HASH_LEN = {CRYPTO_SHA1_HMAC: 20, CRYPTO_SHA2_256_HMAC: 32, CRYPTO_SHA2_384_HMAC: 48, CRYPTO_SHA2_512_HMAC: 64}
 CRYPTO_AES_ICM = 23
 CSP_F_SEPARATE_AAD = 0x2
 CSP_F_ESN = 0x4
@@ -42,6 +45,7 @@ def lib():
         L.oref_sa_free.argtypes = [C.c_void_p]
         L.oref_sha256.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p]
         L.oref_hmac.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_size_t, C.c_void_p]
+        L.oref_hash.argtypes = [C.c_int, C.c_char_p, C.c_size_t, C.c_void_p]
         L.oref_aes_ctr.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_void_p, C.c_int]
         L.oref_esp_decrypt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
         L.oref_esp_encrypt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
@@ -72,7 +76,7 @@ class SA:
     def __init__(self, mode, ckey, salt=b"\0\0\0\0", akey=b"", mlen=0, flags=0,
                  calg=CRYPTO_AES_CBC, aalg=CRYPTO_SHA1_HMAC):
         """ETA: calg CRYPTO_AES_CBC or CRYPTO_AES_ICM (ESP AES-CTR, salt = the
-        RFC 3686 nonce), aalg CRYPTO_SHA1_HMAC or CRYPTO_SHA2_256_HMAC."""
+        RFC 3686 nonce), aalg CRYPTO_SHA1_HMAC or CRYPTO_SHA2_256/384/512_HMAC."""
         self.mode = mode
         self.h = lib().oref_sa_new2(mode, flags, calg, bytes(ckey), len(ckey), bytes(salt),
                                     aalg, bytes(akey), len(akey), mlen)
@@ -119,10 +123,17 @@ def sha256(msg):
     return out.raw
 
 
+def hash(alg, msg):
+    """Plain SHA-1 / SHA-256 / SHA-384 / SHA-512 (alg = the HMAC algorithm id)."""
+    out = C.create_string_buffer(64)
+    lib().oref_hash(alg, bytes(msg), len(msg), out)
+    return out.raw[:HASH_LEN[alg]]
+
+
 def hmac(alg, key, msg):
-    out = C.create_string_buffer(32)
+    out = C.create_string_buffer(64)
     lib().oref_hmac(alg, bytes(key), len(key), bytes(msg), len(msg), out)
-    return out.raw[:32 if alg == CRYPTO_SHA2_256_HMAC else 20]
+    return out.raw[:HASH_LEN[alg]]
 
 
 def aes_ctr(key, ctr16, data):

@@ -12,7 +12,7 @@ plain-data JSON fixtures next to this script:
                      test_cryptodev_aead_test_vectors.h:88-434,1037-1687,1740-1793
   cbc_hmac_sha1.json AES-CBC + HMAC-SHA1 chained KATs (encrypt-then-MAC over CT)
                      test_cryptodev_aes_test_vectors.h:1492,2187,2309
-  eta_esp_packets.json  complete ESP tunnel packets, AES-CBC + HMAC-SHA2-256-128
+  eta_esp_packets.json  complete ESP tunnel packets, AES-CBC + HMAC-SHA2-256/384/512
                      test_cryptodev_security_ipsec_test_vectors.h:744,1721
   ctr_hmac_sha1.json AES-CTR (full 128-bit counter) + HMAC-SHA1 chained KATs
                      test_cryptodev_aes_test_vectors.h:1221,1311,1358,1447
@@ -245,15 +245,19 @@ def cbc_hmac_sha1():
 
 
 def eta_esp_packets():
-    """ESP packets of CBC + HMAC-SHA2-256 SAs (ICV = 16 bytes, RFC 4868)."""
+    """ESP packets of CBC + HMAC-SHA2-256/384/512 SAs (ICV = half the hash,
+    RFC 4868: 16, 24, 32 bytes)."""
     path = os.path.join(TESTDIR, "test_cryptodev_security_ipsec_test_vectors.h")
     structs = parse_structs(path, r"struct\s+ipsec_test_data")
+    modes = {"RTE_CRYPTO_AUTH_SHA256_HMAC": "cbc-hmac-sha256", "RTE_CRYPTO_AUTH_SHA384_HMAC": "cbc-hmac-sha384",
+             "RTE_CRYPTO_AUTH_SHA512_HMAC": "cbc-hmac-sha512"}
     out = []
-    for name in ["pkt_aes_128_cbc_hmac_sha256", "pkt_aes_128_cbc_hmac_sha256_v6"]:
+    for name in ["pkt_aes_128_cbc_hmac_sha256", "pkt_aes_128_cbc_hmac_sha256_v6",
+                 "pkt_aes_128_cbc_hmac_sha384", "pkt_aes_128_cbc_hmac_sha512"]:
         s = structs[name]
         ch = s["xform"]["chain"]
         cipher, auth = ch["cipher"]["cipher"], ch["auth"]["auth"]
-        assert cipher["algo"] == "RTE_CRYPTO_CIPHER_AES_CBC" and auth["algo"] == "RTE_CRYPTO_AUTH_SHA256_HMAC"
+        assert cipher["algo"] == "RTE_CRYPTO_CIPHER_AES_CBC" and auth["algo"] in modes
         outer = s["output_text"]["data"][: s["output_text"]["len"]]
         inner = s["input_text"]["data"][: s["input_text"]["len"]]
         ver = outer[0] >> 4
@@ -261,7 +265,7 @@ def eta_esp_packets():
         out.append({
             "name": name,
             "source": "dpdk/app/test/test_cryptodev_security_ipsec_test_vectors.h",
-            "mode": "cbc-hmac-sha256",
+            "mode": modes[auth["algo"]],
             "cipher_key": hexs(data_of(s["key"], {}, cipher["key"]["length"])),
             "auth_key": hexs(data_of(s["auth_key"], {}, auth["key"]["length"])),
             "digest_len": auth["digest_length"],

@@ -47,10 +47,13 @@ def test_probesession_accepts_esp_gcm(klen):
 
 @pytest.mark.parametrize("calg", [L.CRYPTO_AES_CBC, L.CRYPTO_AES_ICM])
 @pytest.mark.parametrize("aalg,mlen", [(L.CRYPTO_SHA1_HMAC, 12), (L.CRYPTO_SHA2_256_HMAC, 16),
-                                       (L.CRYPTO_SHA2_256_HMAC, 0)])
+                                       (L.CRYPTO_SHA2_256_HMAC, 0), (L.CRYPTO_SHA2_384_HMAC, 24),
+                                       (L.CRYPTO_SHA2_384_HMAC, 48), (L.CRYPTO_SHA2_512_HMAC, 32),
+                                       (L.CRYPTO_SHA2_512_HMAC, 0)])
 def test_probesession_accepts_eta_variants(calg, aalg, mlen):
     """AES-CBC / AES-CTR (enc_xform ivsize 16, xform_aes_icm.c:69) with
-    HMAC-SHA1 or HMAC-SHA2-256 (esp_init, xform_esp.c:225-241)."""
+    HMAC-SHA1 or HMAC-SHA2-256/384/512 (esp_init, xform_esp.c:225-241; ICV
+    up to the hash size, swcr_setup_auth)."""
     for klen in (16, 24, 32):
         assert _probe(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=calg, csp_cipher_klen=klen,
                       csp_cipher_key=b"k" * klen, csp_auth_alg=aalg, csp_auth_klen=32,
@@ -72,7 +75,11 @@ def test_probesession_accepts_esp_cbc_sha1():
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
          csp_auth_alg=9, csp_auth_klen=32),                                                 # auth alg not served
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
-         csp_auth_alg=19, csp_auth_klen=48),                                                # SHA2-384 not served
+         csp_auth_alg=19, csp_auth_klen=48, csp_auth_mlen=52),                              # mlen > SHA-384
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
+         csp_auth_alg=20, csp_auth_klen=64, csp_auth_mlen=30),                              # ICV not dwords
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16,
+         csp_auth_alg=8, csp_auth_klen=20),                                                 # RIPEMD-160 not served
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=12, csp_cipher_alg=23, csp_cipher_klen=16,
          csp_auth_alg=7, csp_auth_klen=20),                                                 # CTR ivlen != 16
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=23, csp_cipher_klen=16,

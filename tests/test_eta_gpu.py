@@ -188,8 +188,13 @@ def test_eta_opencrypto_roundtrip(drv):
 # AES-CTR (RFC 3686) and HMAC-SHA2-256 ETA sessions
 
 def _variant_sas(rng, esn=False):
+    """Every cipher x hash pair; SHA2-384/512 SAs (the MODE 3 launch beside the
+    fused ones) include auth keys longer than the 128-byte block (hashed
+    first, hmac_init_pad) and a short one."""
     return [EtaSA(rng, 16, esn=esn, ctr=c, sha256=h) for c in (False, True) for h in (False, True)] + \
-           [EtaSA(rng, 32, esn=esn, ctr=True, sha256=True), EtaSA(rng, 24, esn=esn, ctr=True)]
+           [EtaSA(rng, 32, esn=esn, ctr=True, sha256=True), EtaSA(rng, 24, esn=esn, ctr=True),
+            EtaSA(rng, 16, esn=esn, sha=384), EtaSA(rng, 24, esn=esn, sha=512),
+            EtaSA(rng, 32, esn=esn, ctr=True, sha=512, aklen=150), EtaSA(rng, 16, esn=esn, ctr=True, sha=384, aklen=7)]
 
 
 def _variant_cts(rng, sas, sa_idx):
@@ -308,26 +313,30 @@ def test_eta_variants_trailer(drv):
         drv.freesession(s)
 
 
-@pytest.mark.parametrize("alg", ["ctr-sha1", "ctr-sha256", "cbc-sha256"])
+@pytest.mark.parametrize("alg", ["ctr-sha1", "ctr-sha256", "cbc-sha256", "cbc-sha384", "ctr-sha512"])
 def test_eta_variants_opencrypto_roundtrip(drv, alg):
     """esp_output -> esp_input through process/flush/poll for the AES-CTR
-    (crp_iv = nonce || IV || be32(1), xform_esp.c:453-458) and HMAC-SHA2-256
+    (crp_iv = nonce || IV || be32(1), xform_esp.c:453-458) and HMAC-SHA2
     SAs: ciphertext and ICV bit-exact vs the oracle, flipped ICV -> EBADMSG."""
-    from espgpu.esp import CBC_SHA256, CTR_SHA1, CTR_SHA256, SecAssoc, esp_input_crp, esp_output_crp, esp_pad
+    from espgpu import esp as E
+    from espgpu.esp import SecAssoc, esp_input_crp, esp_output_crp, esp_pad
     from espgpu.opencrypto import CryptoFramework
     fw = CryptoFramework(drv)
-    rng = np.random.default_rng(1600 + len(alg))
-    ctr, sha256 = alg.startswith("ctr"), alg.endswith("256")
-    name = {"ctr-sha1": CTR_SHA1, "ctr-sha256": CTR_SHA256, "cbc-sha256": CBC_SHA256}[alg]
+    rng = np.random.default_rng(1600 + len(alg) + 7 * alg.endswith("384"))
+    ctr, bits = alg.startswith("ctr"), int(alg.split("sha")[1])
+    name = {"ctr-sha1": E.CTR_SHA1, "ctr-sha256": E.CTR_SHA256, "cbc-sha256": E.CBC_SHA256,
+            "cbc-sha384": E.CBC_SHA384, "ctr-sha512": E.CTR_SHA512}[alg]
+    aalg = {1: O.CRYPTO_SHA1_HMAC, 256: O.CRYPTO_SHA2_256_HMAC, 384: O.CRYPTO_SHA2_384_HMAC,
+            512: O.CRYPTO_SHA2_512_HMAC}[bits]
     ckey = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
     nonce = rng.integers(0, 256, 4, dtype=np.uint8).tobytes() if ctr else b""
-    akey = rng.integers(0, 256, 32 if sha256 else 20, dtype=np.uint8).tobytes()
+    akey = rng.integers(0, 256, {1: 20, 256: 32, 384: 48, 512: 64}[bits], dtype=np.uint8).tobytes()
     sa = SecAssoc(0x5150, name, ckey + nonce, akey)
+    assert sa.mlen == {1: 12, 256: 16, 384: 24, 512: 32}[bits]
     err, ses = fw.crypto_newsession(sa.csp())
     assert err == 0
     orc = O.SA(O.CSP_MODE_ETA, ckey, nonce or b"\0\0\0\0", akey=akey, mlen=sa.mlen,
-               calg=O.CRYPTO_AES_ICM if ctr else O.CRYPTO_AES_CBC,
-               aalg=O.CRYPTO_SHA2_256_HMAC if sha256 else O.CRYPTO_SHA1_HMAC)
+               calg=O.CRYPTO_AES_ICM if ctr else O.CRYPTO_AES_CBC, aalg=aalg)
     pkts, refs = [], []
     for nbytes in (30, 61, 1400, 8900):
         body = esp_pad(rng.integers(0, 256, nbytes, dtype=np.uint8).tobytes(), blocksize=4 if ctr else 16)
@@ -358,13 +367,15 @@ def test_eta_variants_opencrypto_roundtrip(drv, alg):
 
 
 @pytest.mark.parametrize("v", golden("eta_esp_packets.json"), ids=lambda v: v["name"])
-def test_dpdk_cbc_sha256_esp_kat_opencrypto(drv, v):
-    """DPDK's AES-CBC + HMAC-SHA2-256-128 ESP tunnel packets decrypt through
-    the driver path to the expected inner packets."""
-    from espgpu.esp import CBC_SHA256, SecAssoc, esp_input_crp
+def test_dpdk_cbc_sha2_esp_kat_opencrypto(drv, v):
+    """DPDK's AES-CBC + HMAC-SHA2-256-128 / -384-192 / -512-256 ESP tunnel
+    packets decrypt through the driver path to the expected inner packets."""
+    from espgpu import esp as E
+    from espgpu.esp import SecAssoc, esp_input_crp
     from espgpu.opencrypto import CryptoFramework
     fw = CryptoFramework(drv)
-    sa = SecAssoc(v["spi"], CBC_SHA256, bytes.fromhex(v["cipher_key"]), bytes.fromhex(v["auth_key"]))
+    alg = {"cbc-hmac-sha256": E.CBC_SHA256, "cbc-hmac-sha384": E.CBC_SHA384, "cbc-hmac-sha512": E.CBC_SHA512}
+    sa = SecAssoc(v["spi"], alg[v["mode"]], bytes.fromhex(v["cipher_key"]), bytes.fromhex(v["auth_key"]))
     assert sa.mlen == v["digest_len"]
     err, ses = fw.crypto_newsession(sa.csp())
     assert err == 0

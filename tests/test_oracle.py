@@ -225,14 +225,33 @@ def test_sha256_hmac_against_hashlib():
         assert O.hmac(O.CRYPTO_SHA2_256_HMAC, k, m) == hmac.new(k, m, hashlib.sha256).digest()
 
 
+@pytest.mark.parametrize("alg,name", [(O.CRYPTO_SHA2_384_HMAC, "sha384"), (O.CRYPTO_SHA2_512_HMAC, "sha512")])
+def test_sha512_family_vs_hashlib(alg, name):
+    """The oracle's SHA-384 / SHA-512 (128-byte blocks, 128-bit length) and
+    HMAC (key padded to 128 bytes, hashed first when longer) against Python's
+    hashlib at every padding boundary; keys of 1..200 bytes."""
+    rng = np.random.default_rng(9)
+    for n in (0, 1, 111, 112, 113, 127, 128, 129, 239, 240, 1000, 1464):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert O.hash(alg, m) == hashlib.new(name, m).digest()
+        for kl in (1, 48, 64, 128, 129, 200):
+            k = rng.integers(0, 256, kl, dtype=np.uint8).tobytes()
+            assert O.hmac(alg, k, m) == hmac.new(k, m, name).digest()
+
+
+ETA_MODE_AALG = {"cbc-hmac-sha256": O.CRYPTO_SHA2_256_HMAC, "cbc-hmac-sha384": O.CRYPTO_SHA2_384_HMAC,
+                 "cbc-hmac-sha512": O.CRYPTO_SHA2_512_HMAC}
+
+
 @pytest.mark.parametrize("v", golden("eta_esp_packets.json"), ids=lambda v: v["name"])
-def test_eta_sha256_esp_packet_kat(v):
-    """DPDK ESP tunnel packets under AES-CBC + HMAC-SHA2-256-128 (ICV 16 =
-    hashsize/2, xform_ah.c:125-128): decrypt gives the inner packet, encrypt
-    gives back the packet, a flipped ICV bit is EBADMSG with the record
-    untouched."""
+def test_eta_sha2_esp_packet_kat(v):
+    """DPDK ESP tunnel packets under AES-CBC + HMAC-SHA2-256-128 / -384-192 /
+    -512-256 (ICV = hashsize/2, xform_ah.c:125-128): decrypt gives the inner
+    packet, encrypt gives back the packet, a flipped ICV bit is EBADMSG with
+    the record untouched."""
+    assert v["digest_len"] * 2 == {"cbc-hmac-sha256": 32, "cbc-hmac-sha384": 48, "cbc-hmac-sha512": 64}[v["mode"]]
     sa = O.SA(O.CSP_MODE_ETA, bytes.fromhex(v["cipher_key"]), akey=bytes.fromhex(v["auth_key"]),
-              mlen=v["digest_len"], aalg=O.CRYPTO_SHA2_256_HMAC)
+              mlen=v["digest_len"], aalg=ETA_MODE_AALG[v["mode"]])
     rec = bytes.fromhex(v["esp_record"])
     e, out = sa.esp_decrypt(rec)
     assert e == 0
