@@ -50,7 +50,7 @@ namespace {
 constexpr uint32_t LDS_T = 0;          // Td0/Td1 (decrypt) or Te0/Te1 (encrypt), 64 KiB
 constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32 KiB
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
-constexpr uint32_t lds_bytes(int mode) { return mode == 1 ? 65536u : 163840u; }
+constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 ? 65536u : 163840u; }
 
 constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
 constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
@@ -768,9 +768,10 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
-  if (MODE == 1) {
+  if (MODE == 4) {
     fill_pair(lds, LDS_T, p.tpair, tid, WG);
-  } else {
+  } else if (MODE != 1) {                         // MODE 1 (the MAC pass) reads no table
+
     fill_pair(lds, LDS_T, p.dpair, tid, WG);
     fill_pair(lds, LDS_TE, p.tpair, tid, WG);
     for (int idx = tid; idx < 256 * 32; idx += WG)
@@ -818,6 +819,8 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         }
       } else if (MODE == 0 && ((s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR) || wide_hash(s->aalg))) {
         have = false;                                       // another decrypt launch's session
+      } else if (MODE == 4 && (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR)) {
+        have = false;                                       // the other cipher's pass
       } else if (MODE == 3 && !wide_hash(s->aalg)) {
         have = false;                                       // the fused launches' session
       } else {
@@ -841,28 +844,61 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         }
       }
     }
-    if (MODE == 1) {
-      // ---- encrypt: lane = record (the CBC chain is serial; CTR uses the
-      // same loop with independent blocks) ----
+    if (MODE == 4) {
+      // ---- encrypt, cipher pass (one kernel per cipher): lane = record.
+      // The CBC chain is serial (one AES state per lane), so it runs in a
+      // lean kernel (no hash code, few VGPRs, 2 workgroups x 16 waves per
+      // CU) where occupancy hides the round latency; CTR runs 4 blocks at a
+      // time ----
       if (have && valid) {
         const DevSA *s = p.sas + sa;
         uint8_t *rec = p.arena + off;
         const int nr = (int)s->nr;
-        if (s->calg == ESPGPU_CRYPTO_AES_ICM) {
+        if (CKS == CK_CTR) {
           const uint32_t iv0 = *reinterpret_cast<const uint32_t *>(rec + 8);
           const uint32_t iv1 = *reinterpret_cast<const uint32_t *>(rec + 12);
-          for (uint32_t b = 0; b < (plen + 15) / 16; ++b) {
-            const uint4 ks = aes_enc(make_uint4(salt, iv0, iv1, bswap32(b + 1)), s->rk, nr, lds, slot);
-            st_partial(rec + 16 + 16 * b, xor4(ld16(rec + 16 + 16 * b), ks), (int)(plen - 16 * b));
+          const uint32_t nb = (plen + 15) / 16;
+          for (uint32_t b = 0; b < nb; b += 4) {
+            uint4 ks[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ks[k] = make_uint4(salt, iv0, iv1, bswap32(b + (uint32_t)k + 1));
+            aes_enc4(ks, kp(s->rk), nr, lds, slot);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (b + k < nb)
+                st_partial(rec + 16 + 16 * (b + k), xor4(ld16(rec + 16 + 16 * (b + k)), ks[k]),
+                           (int)(plen - 16 * (b + k)));
           }
         } else {
+          // four blocks (64 contiguous bytes) per load and per store: the
+          // record is streamed in 64-byte pieces, not 16
           uint4 prev = ld16(rec + 8);                       // IV
-          for (uint32_t b = 0; b < plen / 16; ++b) {
-            const uint4 c = aes_enc(xor4(ld16(rec + 24 + 16 * b), prev), s->rk, nr, lds, slot);
-            st16(rec + 24 + 16 * b, c);
-            prev = c;
+          const uint32_t nb = plen / 16;
+          for (uint32_t b = 0; b < nb; b += 4) {
+            uint4 m[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[k] = b + k < nb ? ld16(rec + 24 + 16 * (b + k)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if (b + k < nb) {
+                prev = aes_enc(xor4(m[k], prev), s->rk, nr, lds, slot);
+                m[k] = prev;
+              }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (b + k < nb) st16(rec + 24 + 16 * (b + k), m[k]);
           }
         }
+      }
+      continue;
+    }
+    if (MODE == 1) {
+      // ---- encrypt, MAC pass (after MODE 4 wrote the ciphertext): HMAC over
+      // SPI|SN|IV|CT (|ESN), ICV = its first mlen bytes ----
+      if (have && valid) {
+        const DevSA *s = p.sas + sa;
+        uint8_t *rec = p.arena + off;
         uint32_t dg[16];
         hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
                  kp(s->opad), dg);
@@ -998,15 +1034,22 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *strea
   }
   const int two_pass = !encrypt && p.out == p.arena;
   if (encrypt) {
+    // cipher passes (lean, 1024 threads, up to 2 workgroups per CU), then the
+    // MAC pass; kinds: bits 0/2 = CBC sessions (SHA-1/256, SHA-384/512),
+    // bits 1/3 = CTR sessions
+    const int g4 = p.chunks == nullptr ? std::max(1, std::min(2 * grid, (int)(((p.n + 63) / 64 + 15) / 16)))
+                                       : 2 * grid;
+    if (kinds & 5) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(g4), dim3(1024), 0, st, p);
+    if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(g4), dim3(1024), 0, st, p);
     hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(grid), dim3(768), 0, st, p);
   } else if (two_pass) {
     hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(grid), dim3(768), 0, st, p);
   } else {
     // kinds: bit 0 = SHA-1 / SHA2-256 CBC sessions exist, bit 1 = such CTR
-    // sessions, bit 2 = SHA2-384/512 sessions (either cipher)
+    // sessions, bits 2/3 = SHA2-384/512 CBC / CTR sessions
     if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(grid), dim3(768), 0, st, p);
     if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(grid), dim3(768), 0, st, p);
-    if (kinds & 4) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(grid), dim3(768), 0, st, p);
+    if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(grid), dim3(768), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -95,9 +95,9 @@ struct espgpu_ctx {
   uint32_t *d_queue = nullptr;   // work queues: [0..1] GCM, [2..3] ETA (ticket, retired; self-resetting)
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
-  // ETA sessions: all, and by decrypt kernel: narrow-hash (SHA-1 / SHA2-256)
-  // CBC, narrow-hash CTR, wide-hash (SHA2-384/512, either cipher)
-  int n_eta = 0, n_cbc = 0, n_ctr = 0, n_wide = 0;
+  // ETA sessions: all, and by kernel: narrow-hash (SHA-1 / SHA2-256) CBC and
+  // CTR, wide-hash (SHA2-384/512) CBC and CTR
+  int n_eta = 0, n_cbc = 0, n_ctr = 0, n_wcbc = 0, n_wctr = 0;
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -268,7 +268,8 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.isbox = c->d_isbox;
     q.status = d_status;
     q.nsas = nsas;
-    const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wide > 0 ? 4 : 0);
+    const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wcbc > 0 ? 4 : 0) |
+                   (c->n_wctr > 0 ? 8 : 0);
     if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, st)) return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
@@ -476,9 +477,8 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
       hc::hmac_sha1_pad_state(ak, csp->csp_auth_klen, 0x5c, sa.opad);
     }
     c->n_eta++;
-    if (wide) c->n_wide++;
-    else if (csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM) c->n_ctr++;
-    else c->n_cbc++;
+    const bool ctr = csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
+    (wide ? (ctr ? c->n_wctr : c->n_wcbc) : (ctr ? c->n_ctr : c->n_cbc))++;
   }
   HIPCHK(c, hipMemcpy(c->d_sas + slot, &sa, sizeof sa, hipMemcpyHostToDevice));
   Session &s = c->sessions[slot];
@@ -506,9 +506,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   const Session &fs = c->sessions[sid];
   if (fs.mode == ESPGPU_CSP_MODE_ETA) {
     c->n_eta--;
-    if (fs.wide) c->n_wide--;
-    else if (fs.ctr) c->n_ctr--;
-    else c->n_cbc--;
+    (fs.wide ? (fs.ctr ? c->n_wctr : c->n_wcbc) : (fs.ctr ? c->n_ctr : c->n_cbc))--;
   }
   c->sessions[sid] = Session();
   DevSA z;
