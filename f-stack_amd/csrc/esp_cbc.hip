@@ -50,7 +50,7 @@ namespace {
 constexpr uint32_t LDS_T = 0;          // Td0/Td1 (decrypt) or Te0/Te1 (encrypt), 64 KiB
 constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32 KiB
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
-constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 ? 65536u : 163840u; }
+constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode == 6 ? 65536u : 163840u; }
 
 constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
 constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
@@ -770,7 +770,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
   if (MODE == 4) {
     fill_pair(lds, LDS_T, p.tpair, tid, WG);
-  } else if (MODE != 1) {                         // MODE 1 (the MAC pass) reads no table
+  } else if (MODE != 1 && MODE != 6) {            // MODE 1 / 6 (MAC passes) read no table
 
     fill_pair(lds, LDS_T, p.dpair, tid, WG);
     fill_pair(lds, LDS_TE, p.tpair, tid, WG);
@@ -823,6 +823,8 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         have = false;                                       // the other cipher's pass
       } else if (MODE == 3 && !wide_hash(s->aalg)) {
         have = false;                                       // the fused launches' session
+      } else if ((MODE == 5 || MODE == 6) && wide_hash(s->aalg)) {
+        have = false;                                       // MODE 3's session
       } else {
         const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;
         const uint32_t mlen = s->mlen;
@@ -832,11 +834,21 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         // blocksize (16 for CBC, 1 for CTR; records are 4-byte multiples)
         valid = pl > 0 && (ctr || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
-        if (valid && (MODE == 2 || MODE == 3)) {
+        if (valid && MODE == 5) ok = p.status[di] == ESPGPU_OK;   // verified by the MODE 6 pass
+        if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
-          hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
-                   kp(s->opad), dg);
+          if (MODE == 6) {              // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
+            if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+              hmac_t<HS_SHA256>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                                kp(s->opad), dg);
+            else
+              hmac_t<HS_SHA1>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                              kp(s->opad), dg);
+          } else {
+            hmac_any((int)s->aalg, rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                     kp(s->opad), dg);
+          }
           uint32_t diff = 0;
           for (uint32_t k = 0; k < mlen / 4; ++k)
             diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
@@ -934,7 +946,11 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       if (have && p.trailer && !valid) p.trailer[di] = 0;
       continue;
     }
-    if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+    if (MODE == 6) {                // verify pass: status only; MODE 5 decrypts what passed
+      if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+      continue;
+    }
+    if (have && MODE != 5) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
     // trailer word: 0 now for records that will not be decrypted; the lane
     // decrypting a record's last block writes the others'
     if (have && p.trailer && !(valid && ok)) p.trailer[di] = 0;
@@ -966,40 +982,67 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       const uint32_t start = incl - nb;
       const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
       const int nr = (int)s->nr;
-      for (int base = total - 64; base > -64; base -= 64) {
-        const int f = base + lane;
-        // the record holding flat block f: the last lane whose start <= f
-        int j = 0;
-        uint32_t sj = 0;
+      // U blocks per lane per pass, 64 apart (each load instruction covers
+      // 64 consecutive blocks), decrypted together for ILP
+      constexpr int U = 4;
+      for (int base = total - 64 * U; base > -64 * U; base -= 64 * U) {
+        int fk[U];
+        uint32_t ik[U], rok[U], rplk[U], rdik[U], rsk[U];
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-          const uint32_t sc = __shfl(start, j + step);
-          if ((int)sc <= f) {
-            j += step;
-            sj = sc;
+        for (int k = 0; k < U; ++k) {
+          const int f = base + lane + 64 * k;
+          // the record holding flat block f: the last lane whose start <= f
+          int j = 0;
+          uint32_t sj = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1) {
+            const uint32_t sc = __shfl(start, j + step);
+            if ((int)sc <= f) {
+              j += step;
+              sj = sc;
+            }
+          }
+          fk[k] = f;
+          ik[k] = (uint32_t)f - sj;
+          rok[k] = __shfl(off, j);
+          rplk[k] = __shfl(plen, j);
+          rdik[k] = __shfl(di, j);
+          rsk[k] = __shfl(salt, j);
+        }
+        // all loads of the pass before any store (in place: see above)
+        uint4 v[U], pv[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          v[k] = pv[k] = make_uint4(0, 0, 0, 0);
+          if (fk[k] >= 0) {
+            const uint8_t *rec = p.arena + rok[k];
+            if (ctr) {
+              pv[k] = ld16(rec + 16 + 16 * ik[k]);                                   // C_i
+              v[k] = make_uint4(rsk[k], *reinterpret_cast<const uint32_t *>(rec + 8),
+                                *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(ik[k] + 1));
+            } else {
+              v[k] = ld16(rec + 24 + 16 * ik[k]);                                    // C_i
+              pv[k] = ld16(rec + 8 + 16 * ik[k]);                // C_{i-1}, or the IV for i = 0
+            }
           }
         }
-        const uint32_t ro = __shfl(off, j);
-        const uint32_t rpl = __shfl(plen, j), rdi = __shfl(di, j), rsalt = __shfl(salt, j);
-        if (f >= 0) {
-          const uint32_t i = (uint32_t)f - sj;
-          const uint8_t *rec = p.arena + ro;
-          uint8_t *dst = (MODE == 3 ? p.out : p.arena) + ro;   // MODE 3: out of place
-          const int rem = (int)rpl - 16 * (int)i;
-          uint4 pt;
-          if (ctr) {
-            const uint4 c = ld16(rec + 16 + 16 * i);
-            const uint4 cb = make_uint4(rsalt, *reinterpret_cast<const uint32_t *>(rec + 8),
-                                        *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(i + 1));
-            pt = xor4(c, aes_enc(cb, kp(s->rk), nr, lds + LDS_TE, slot));
-            st_partial(dst + 16 + 16 * i, pt, rem);
-          } else {
-            const uint4 c = ld16(rec + 24 + 16 * i);
-            const uint4 prev = ld16(rec + 8 + 16 * i);       // C_{i-1}, or the IV for i = 0
-            pt = xor4(aes_dec(c, kp(s->dk), nr, lds, slot), prev);
-            st16(dst + 24 + 16 * i, pt);
+        if (ctr)
+          aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
+        else
+          aes_dec4(v, kp(s->dk), nr, lds, slot);
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          if (fk[k] >= 0) {
+            uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3 / 5: p.out (may be p.arena)
+            const uint32_t i = ik[k], rpl = rplk[k];
+            const int rem = (int)rpl - 16 * (int)i;
+            const uint4 pt = xor4(v[k], pv[k]);
+            if (ctr)
+              st_partial(dst + 16 + 16 * i, pt, rem);
+            else
+              st16(dst + 24 + 16 * i, pt);
+            if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdik[k]] = esp_trailer_word(last_word(pt, rem), rpl);
           }
-          if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdi] = esp_trailer_word(last_word(pt, rem), rpl);
         }
       }
     }
@@ -1024,32 +1067,42 @@ int set_eta_opts(uint32_t opts) {
 
 // 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
 // schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
-int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream) {
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   // implicit units (64 records, one wave each): no more workgroups than units
-  if (p.chunks == nullptr) {
-    const int units = (int)((p.n + 63) / 64), wpg = 768 / 64;
-    grid = std::max(1, std::min(grid, (units + wpg - 1) / wpg));
-  }
-  const int two_pass = !encrypt && p.out == p.arena;
+  auto clamp = [&](int g, int wg) {
+    if (p.chunks != nullptr) return g;
+    const int units = (int)((p.n + 63) / 64), wpg = wg / 64;
+    return std::max(1, std::min(g, (units + wpg - 1) / wpg));
+  };
+  const int in_place = !encrypt && p.out == p.arena;
+  // kinds: bit 0 = SHA-1 / SHA2-256 CBC sessions exist, bit 1 = such CTR
+  // sessions, bits 2/3 = SHA2-384/512 CBC / CTR sessions
   if (encrypt) {
-    // cipher passes (lean, 1024 threads, up to 2 workgroups per CU), then the
-    // MAC pass; kinds: bits 0/2 = CBC sessions (SHA-1/256, SHA-384/512),
-    // bits 1/3 = CTR sessions
-    const int g4 = p.chunks == nullptr ? std::max(1, std::min(2 * grid, (int)(((p.n + 63) / 64 + 15) / 16)))
-                                       : 2 * grid;
-    if (kinds & 5) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(g4), dim3(1024), 0, st, p);
-    if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(g4), dim3(1024), 0, st, p);
-    hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(grid), dim3(768), 0, st, p);
-  } else if (two_pass) {
-    hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(grid), dim3(768), 0, st, p);
+    // cipher passes (lean, 1024 threads, up to 2 workgroups per CU), then the MAC pass
+    if (kinds & 5) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
+    if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
+    hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+  } else if (fused) {
+    // round-1/2 layout: one fused pass per cipher (out of place) or the
+    // verify-first kernel (in place)
+    if (in_place) {
+      hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    } else {
+      if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    }
   } else {
-    // kinds: bit 0 = SHA-1 / SHA2-256 CBC sessions exist, bit 1 = such CTR
-    // sessions, bits 2/3 = SHA2-384/512 CBC / CTR sessions
-    if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(grid), dim3(768), 0, st, p);
-    if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(grid), dim3(768), 0, st, p);
-    if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(grid), dim3(768), 0, st, p);
+    // verify pass (lane = record HMAC, status), then the block-parallel
+    // decrypt of the records that passed, in place or out of place: two lean
+    // kernels, each at the occupancy its own registers allow
+    if (kinds & 3) {
+      hipLaunchKernelGGL((eta_kernel<6, 768, -1>), dim3(clamp(2 * grid, 768)), dim3(768), 0, st, p);
+      hipLaunchKernelGGL((eta_kernel<5, 1024, -1>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
+    }
+    if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

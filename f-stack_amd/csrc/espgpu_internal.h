@@ -113,7 +113,9 @@ int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *st
 int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
 int set_eta_opts(uint32_t opts);
 // kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones
-int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream);
+// fused: 1 = the one-pass out-of-place decrypt (MODE 0) / verify-first
+// in-place kernel (MODE 2); 0 = verify pass + block-parallel decrypt pass
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream);

@@ -215,14 +215,17 @@ def _mask_var(descs, size, hl, ml):
     return m
 
 
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("esn", [False, True])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace):
-    """AES-CBC / AES-CTR x HMAC-SHA1-96 / HMAC-SHA2-256-128 sessions mixed in
-    one batch (planner path), AES-128/192/256, tag failures anywhere in the
+def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
+    """AES-CBC / AES-CTR x HMAC-SHA1-96 / HMAC-SHA2 sessions mixed in one
+    batch (planner path), AES-128/192/256, tag failures anywhere in the
     record: statuses and plaintext bit-exact vs the oracle, failed records
-    untouched in place."""
+    untouched in place.  fused=0: the separate verify + block-decrypt kernels
+    (set_tuning eta_fused)."""
     from espgpu.batch import decrypt_batch
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
     rng = np.random.default_rng(1300 + 2 * esn + inplace)
     sas = _variant_sas(rng, esn)
     sids = _sessions(drv, sas)
@@ -257,6 +260,7 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace):
         assert (res[m_bad] == bad[m_bad]).all()
     for s in sids:
         drv.freesession(s)
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 1) == 0
 
 
 def test_eta_variants_encrypt_vs_oracle(drv):
