@@ -574,11 +574,23 @@ __device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
 // whose ICV fails too; the status byte says so, as in the GCM kernel).
 // Returns whether the first mlen bytes of the HMAC match the ICV; *trl gets
 // the esp_input_cb trailer word from the last block.
+// Per-wave 4 KiB staging tile for the plaintext of the full chunks: (record
+// r of the wave, 16-byte part k) at bank line 4*(r>>4) + k, slot
+// 4*((p+q)&3) + ((k+q)&3) with u = r&15, p = u>>2, q = u&3.  Conflict-free
+// per 16-lane group both for a lane writing its own record's part k and for
+// 4-lane groups reading one record's 64 contiguous bytes.
+__device__ __forceinline__ uint32_t tile_off(int r, int k) {
+  const int u = r & 15, pp = u >> 2, q = u & 3;
+  return (uint32_t)(((r >> 4) * 4 + k) * 256 + (4 * ((pp + q) & 3) + ((k + q) & 3)) * 16);
+}
+
 template <int CK, int HS>
 __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *orec, uint32_t plen, uint32_t mlen, bool esn,
                                   uint32_t esn_hi, uint32_t salt, kptr ipad, kptr opad, kptr key, int nr,
-                                  const uint8_t *lds, uint32_t slot, bool act, uint32_t *trl) {
+                                  const uint8_t *lds, uint8_t *tile, uint8_t *out, uint32_t off, uint32_t slot,
+                                  bool act, uint32_t *trl) {
   constexpr int W = Hash<HS>::W;
+  const int lane = threadIdx.x & 63, qb = lane & ~3, pi = lane & 3;
   constexpr uint32_t HL = CK == CK_CBC ? 24u : 16u;
   const uint32_t L0 = HL + plen, L = L0 + (esn ? 4u : 0u);
   const uint32_t nfull = L0 / 64, total = (L + 9 + 63) / 64, nct = (plen + 15) / 16;
@@ -595,7 +607,8 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
   for (uint32_t b = 0; b <= T; ++b) {
     const bool on = act && b <= total;
     uint32_t w[16];
-    if (on && b < nfull) {
+    const bool full = on && b < nfull;
+    if (full) {
       uint32_t m[16];
       const uint8_t *q = rec + 64 * b;
 #pragma unroll
@@ -627,8 +640,9 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
         if (!(eopts() & 2)) aes_dec4(d, key, nr, lds, slot);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if (k < nb && !(eopts() & 8)) {
-            st16(orec + HL + 16 * (i0 + k), xor4(d[k], prev));
+          if (k < nb) {
+            // to the tile; stored below 4 lanes per record
+            *reinterpret_cast<uint4 *>(tile + tile_off(lane, k)) = xor4(d[k], prev);
             prev = blk[k];
           }
         }
@@ -643,9 +657,9 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
         if (!(eopts() & 2)) aes_enc4(ks, key, nr, te, slot);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          if ((b > 0 || k > 0) && !(eopts() & 8))               // chunk 0 starts with SPI|SN|IV
-            st16(orec + HL + 16 * (4 * b - 1 + (uint32_t)k),
-                 xor4(make_uint4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]), ks[k]));
+          if (b > 0 || k > 0)                                      // chunk 0 starts with SPI|SN|IV
+            *reinterpret_cast<uint4 *>(tile + tile_off(lane, b > 0 ? k : k - 1)) =
+                xor4(make_uint4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]), ks[k]);
         }
       }
 #pragma unroll
@@ -715,6 +729,22 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
 #pragma unroll
       for (int k = 0; k < W; ++k) h[k] = hn[k];
     }
+    // chunk b's plaintext out of the tile, 4 lanes x 16 contiguous bytes per
+    // record: CBC blocks 4b-2 .. 4b+1 (0, 1 for b = 0) are record bytes
+    // [64b-8, 64b+56), CTR blocks 4b-1 .. 4b+2 (0..2) bytes [64b, 64b+64).
+    // Lane = record stores (16 B at 64 records per instruction) write the
+    // same lines in 4x the pieces and leave them half-written in L2.
+    if (!(eopts() & 8)) {
+      const uint32_t obase = CK == CK_CBC ? (b == 0 ? 24u : 64 * b - 8) : (b == 0 ? 16u : 64 * b);
+      const int np = CK == CK_CBC ? (b == 0 ? 2 : 4) : (b == 0 ? 3 : 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int src = qb | t;
+        const uint32_t soff = (uint32_t)__shfl((int)off, src);
+        if (__shfl((int)full, src) && pi < np)
+          st16(out + soff + obase + 16 * pi, *reinterpret_cast<const uint4 *>(tile + tile_off(src, pi)));
+      }
+    }
   }
   uint32_t diff = 0;
   if (act)
@@ -726,13 +756,13 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
 template <int CK>
 __device__ __forceinline__ bool fused_hs(int aalg, const uint8_t *rec, uint8_t *orec, uint32_t plen,
                                          uint32_t mlen, bool esn, uint32_t esn_hi, uint32_t salt, kptr ipad,
-                                         kptr opad, kptr key, int nr, const uint8_t *lds, uint32_t slot, bool act,
-                                         uint32_t *trl) {
+                                         kptr opad, kptr key, int nr, const uint8_t *lds, uint8_t *tile, uint8_t *out,
+                                         uint32_t off, uint32_t slot, bool act, uint32_t *trl) {
   if (aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
     return eta_decrypt_fused<CK, HS_SHA256>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds,
-                                            slot, act, trl);
-  return eta_decrypt_fused<CK, HS_SHA1>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds, slot,
-                                        act, trl);
+                                            tile, out, off, slot, act, trl);
+  return eta_decrypt_fused<CK, HS_SHA1>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds, tile,
+                                        out, off, slot, act, trl);
 }
 
 // out: the digest as big-endian words (5 / 8 / 12 / 16 of them)
@@ -771,12 +801,18 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   if (MODE == 4) {
     fill_pair(lds, LDS_T, p.tpair, tid, WG);
   } else if (MODE != 1 && MODE != 6) {            // MODE 1 / 6 (MAC passes) read no table
-
-    fill_pair(lds, LDS_T, p.dpair, tid, WG);
-    fill_pair(lds, LDS_TE, p.tpair, tid, WG);
-    for (int idx = tid; idx < 256 * 32; idx += WG)
-      *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[idx >> 5];
+    // a MODE 0 kernel serves one cipher: CBC needs Td + the inverse S-box and
+    // stages plaintext where Te would be, CTR needs Te and stages in Td's place
+    if (MODE != 0 || CKS != CK_CTR) {
+      fill_pair(lds, LDS_T, p.dpair, tid, WG);
+      for (int idx = tid; idx < 256 * 32; idx += WG)
+        *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[idx >> 5];
+    }
+    if (MODE != 0 || CKS != CK_CBC) fill_pair(lds, LDS_TE, p.tpair, tid, WG);
   }
+  static_assert((WG / 64) * 4096 <= 65536, "plaintext tiles fit the unused table region");
+  uint8_t *tile = lds + (CKS == CK_CTR ? LDS_T : LDS_TE) +
+                  (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6) * 4096u;   // wave-uniform (MODE 0)
   __syncthreads();
 
   // Work units are one wave's worth of records: a 64-record ETA chunk of one
@@ -936,7 +972,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         const uint32_t roff = (eopts() & 1) ? (off & 0xffffcu) : off;
         const bool good = fused_hs<CKS == CK_CTR ? CK_CTR : CK_CBC>(
             (int)s->aalg, p.arena + roff, p.out + roff, plen, s->mlen, esn, esnh, salt, kp(s->ipad), kp(s->opad),
-            kp(CKS == CK_CTR ? s->rk : s->dk), (int)s->nr, lds, slot, mine, &trl);
+            kp(CKS == CK_CTR ? s->rk : s->dk), (int)s->nr, lds, tile, p.out, roff, slot, mine, &trl);
         if (mine) {
           ok = good;
           if (p.trailer) p.trailer[di] = good ? trl : 0u;
