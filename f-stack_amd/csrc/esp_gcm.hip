@@ -20,10 +20,9 @@
 //    XOR-reduced across the lane group.  Multiplication by a fixed H^e uses
 //    tables indexed per byte or nibble POSITION, so there is no shift/reduce
 //    step: X*H^e = XOR_j T_e[j][digit_j(X)].  The Horner multiplier H^S is in
-//    LDS with 8-bit indices (16 ds_read_b128 per block); the per-lane final
-//    H^(S-l) is gathered from L2 (4-bit tables).  Measured against a
-//    conflict-free 4-bit layout with four T-tables: this layout
-//    reads half the GHASH rows, which outweighs its bank conflicts.
+//    LDS with 8-bit indices (16 ds_read_b128 per block, value-major and read
+//    in a lane-dependent position order, so conflict-free: gf_mul8); the
+//    per-lane final H^(S-l) is gathered from L2 (4-bit tables).
 //  * AES-CTR uses T-tables Te0 and Te1 replicated 32x in LDS (entry x at x*256:
 //    Te0 in lane slots (lane&31)*4, Te1 128 bytes later): ds_read_b32 with every
 //    lane of a 32-lane group on its own bank -> conflict-free; the LDS address
@@ -49,9 +48,9 @@ namespace espgpu {
 
 namespace {
 
-// LDS: the 8-bit H^8 GHASH table at 0 (so its 16 position offsets p*4096
-// fit the DS instructions' 16-bit immediate), the AES T-table at 64 KiB.
-constexpr uint32_t LDS_GT = 0;          // H^8, 16 positions x 256 values x 16 B
+// LDS: the 8-bit H^S GHASH table at 0 (value-major, gf_mul8), the AES
+// T-table at 64 KiB.
+constexpr uint32_t LDS_GT = 0;          // H^S, 256 values x 16 positions x 16 B
 constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
 constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
 constexpr int S = kGcmLanesPerRec;      // lanes per record
@@ -278,22 +277,52 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32
 }
 
 // ---- GHASH multiply by a fixed power (gf_mul, gfmult.c:219-229) ----------
-// Y * H^8 with 8-bit tables in LDS: 16 lookups (one per byte position p, the
-// row p*4096 + byte*16), XOR-accumulated.  The address is one shift of the
-// byte; the position offset is the DS immediate.  Entry v of a row sits in
-// bank group v mod 16, so lanes of a ds_read_b128 group conflict only when
-// their bytes differ but agree mod 16.
-__device__ __forceinline__ uint4 gf_mul8(uint4 x, const uint8_t *lds) {
+// Y * H^S with 8-bit tables in LDS: 16 lookups, one per byte position p, of the
+// 16-byte product (the block whose byte p is v) * H^S, XOR-accumulated.
+//
+// Bank-conflict-free by construction.  A ds_read_b128 is serviced in four
+// 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32) and
+// its bank quad is address bits 4..7.  The table is value-major, entry (v, p)
+// at v*256 + p*16 (host_crypto.cpp ghash_tables), and in lookup t lane L reads
+// position p = t ^ (L & 15): the 16 lanes of every group have distinct L & 15,
+// so they hit 16 distinct quads whatever their data (a position-major table
+// puts entry v on quad v mod 16: random bytes made 2-4-way conflicts, a quarter
+// of all LDS cycles).  Each lane walks its positions in its own order: its Y
+// words are permuted by (L >> 2) & 3 and the bytes inside each word by L & 3,
+// then each address is one v_perm of (value byte, position << 4).
+struct GhLane {
+  uint32_t selb;      // v_perm selector: byte b <- byte b ^ (L & 3)
+  uint32_t cpos0;     // byte b: (b ^ (L & 15)) << 4 (positions 0..3 of word 0)
+  bool sw1, sw2;      // lane bits 2 and 3: the word permutation
+};
+
+__device__ __forceinline__ GhLane gh_lane(int lane) {
+  GhLane g;
+  const uint32_t jl = (uint32_t)lane & 3u, jj = (uint32_t)lane & 15u;
+  g.selb = (0u ^ jl) | ((1u ^ jl) << 8) | ((2u ^ jl) << 16) | ((3u ^ jl) << 24);
+  g.cpos0 = ((0u ^ jj) << 4) | (((1u ^ jj) << 4) << 8) | (((2u ^ jj) << 4) << 16) | (((3u ^ jj) << 4) << 24);
+  g.sw1 = (lane & 4) != 0;
+  g.sw2 = (lane & 8) != 0;
+  return g;
+}
+
+__device__ __forceinline__ uint4 gf_mul8(uint4 x, const uint8_t *lds, const GhLane &g) {
+  // slot k <- word k ^ ((L >> 2) & 3)
+  const uint32_t a0 = g.sw1 ? x.y : x.x, a1 = g.sw1 ? x.x : x.y;
+  const uint32_t a2 = g.sw1 ? x.w : x.z, a3 = g.sw1 ? x.z : x.w;
+  const uint32_t w[4] = {g.sw2 ? a2 : a0, g.sw2 ? a3 : a1, g.sw2 ? a0 : a2, g.sw2 ? a1 : a3};
   uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
+    // byte b of c = byte b ^ (L & 3) of slot k: position p = (4k + b) ^ (L & 15)
+    const uint32_t c = perm(w[k], w[k], g.selb);
+    const uint32_t cp = g.cpos0 ^ ((uint32_t)k * 0x40404040u);    // p << 4, bytes 0..3
 #pragma unroll
-    for (int q = 0; q < 4; q += 2) {
-      const uint32_t a = ((w[k] >> (8 * q)) & 0xffu) << 4;
-      const uint32_t b = ((w[k] >> (8 * q + 8)) & 0xffu) << 4;
-      const uint4 e = *reinterpret_cast<const uint4 *>(lds + LDS_GT + (4 * k + q) * 4096 + a);
-      const uint4 f = *reinterpret_cast<const uint4 *>(lds + LDS_GT + (4 * k + q + 1) * 4096 + b);
+    for (int b = 0; b < 4; b += 2) {
+      const uint32_t ea = perm(c, cp, 0x0c0c0000u | ((4u + b) << 8) | (uint32_t)b);
+      const uint32_t eb = perm(c, cp, 0x0c0c0000u | ((5u + b) << 8) | (uint32_t)(b + 1));
+      const uint4 e = *reinterpret_cast<const uint4 *>(lds + LDS_GT + ea);
+      const uint4 f = *reinterpret_cast<const uint4 *>(lds + LDS_GT + eb);
       r0 = xor3(r0, e.x, f.x);
       r1 = xor3(r1, e.y, f.y);
       r2 = xor3(r2, e.z, f.z);
@@ -358,6 +387,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   const int l = lane & (S - 1);
   const uint32_t slot = ((uint32_t)(lane & 31) * 4) | (LDS_TP & 0xff0000u);
   const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
+  const GhLane gl = gh_lane(lane);
 
   // -- descriptor and record header ------------------------------------------
   int valid = 0, ct_len = 0, nct = 0, N = 0, M = 0, pad = 0;
@@ -455,11 +485,11 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         }
         const uint4 Bb = block_in(ib, hcb, Cb, kb);
         // M >= m+2: Y = (Y*H^8 ^ Ba)*H^8 ^ Bb;  M == m+1: Y = Y*H^8 ^ Ba
-        const uint4 P = (gopts() & 2) ? Y : gf_mul8(Y, lds);
+        const uint4 P = (gopts() & 2) ? Y : gf_mul8(Y, lds, gl);
         if (M >= m + 1) {
           const uint4 Ym = xor4(P, Ba);
           Y = Ym;
-          if (M >= m + 2) Y = xor4((gopts() & 2) ? Ym : gf_mul8(Ym, lds), Bb);
+          if (M >= m + 2) Y = xor4((gopts() & 2) ? Ym : gf_mul8(Ym, lds, gl), Bb);
         }
         m += 2;
         continue;
@@ -474,7 +504,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
     uint4 ks = make_uint4(0, 0, 0, 0);
     if (m > 0) {
-      const uint4 Yn = gf_mul8(Y, lds);
+      const uint4 Yn = gf_mul8(Y, lds, gl);
       if (m < M) Y = Yn;
     }
     if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);

@@ -39,8 +39,9 @@ static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 //                      at j*256 + n*16; read from L2 by the per-record final
 //                      multiply by H^(8-l);
 // [kGh8Off, +64 KiB)   H^S with 8-bit indices (S = kGcmLanesPerRec): byte
-//                      position p, value v at p*4096 + v*16 (staged into LDS,
-//                      the Horner multiplier).
+//                      position p, value v at v*256 + p*16 (value-major, so
+//                      a row's 16 positions sit in the 16 bank quads; staged
+//                      into LDS, the Horner multiplier, esp_gcm.hip gf_mul8).
 constexpr int kGcmLanesPerRec = 4;                               // GCM kernel: lanes per record
 constexpr uint32_t kGhPowerBytes = 32 * 16 * 16;                 // 8192
 constexpr uint32_t kGh8Off = 8 * kGhPowerBytes;

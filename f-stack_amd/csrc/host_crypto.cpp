@@ -157,8 +157,9 @@ void ghash_tables(const uint8_t h[16], int stride, uint8_t *out) {
   //   power p, nibble position j (byte j>>1, low nibble if j even), value n
   //   at p*8192 + j*256 + n*16 = (the block whose nibble j is n) * H^(p+1).
   // Section 2 (at 64 KiB): H^S with 8-bit indices (S = kGcmLanesPerRec, the
-  //   GCM kernel's Horner stride): byte position q, value v at q*4096 + v*16
-  //   = (the block whose byte q is v) * H^S.
+  //   GCM kernel's Horner stride): byte position q, value v at v*256 + q*16
+  //   = (the block whose byte q is v) * H^S.  Value-major: the 16 positions
+  //   of one value fill one 256-byte LDS row, one position per bank quad.
   uint8_t pw[8][16];
   memcpy(pw[0], h, 16);
   for (int p = 1; p < 8; ++p) gf128_mul(pw[p - 1], h, pw[p]);
@@ -188,7 +189,7 @@ void ghash_tables(const uint8_t h[16], int stride, uint8_t *out) {
     for (int v = 0; v < 256; ++v) {
       const uint8_t *lo = h8 + (2 * q) * 256 + (v & 15) * 16;
       const uint8_t *hi = h8 + (2 * q + 1) * 256 + (v >> 4) * 16;
-      for (int k = 0; k < 16; ++k) t8[(size_t)q * 4096 + (size_t)v * 16 + k] = lo[k] ^ hi[k];
+      for (int k = 0; k < 16; ++k) t8[(size_t)v * 256 + (size_t)q * 16 + k] = lo[k] ^ hi[k];
     }
 }
 

@@ -20,10 +20,10 @@ static_assert(kGhTableBytes == 131072, "layout");
 
 static void xor16(uint8_t *a, const uint8_t *b) { for (int i = 0; i < 16; ++i) a[i] ^= b[i]; }
 
-// as gf_mul8: byte position p (memory order) indexes row p*4096 + byte*16
+// as gf_mul8: byte position p (memory order), value v at v*256 + p*16
 static void mul8(const uint8_t *tab, const uint8_t x[16], uint8_t out[16]) {
   memset(out, 0, 16);
-  for (int p = 0; p < 16; ++p) xor16(out, tab + p * 4096 + x[p] * 16);
+  for (int p = 0; p < 16; ++p) xor16(out, tab + x[p] * 256 + p * 16);
 }
 // as gf_mul4_global: nibble position j = 2p (low) / 2p+1 (high), row j*256
 static void mul4(const uint8_t *t, const uint8_t x[16], uint8_t out[16]) {
