@@ -470,6 +470,35 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
       if (__all((int)(cb >> 8) == cc.hi)) {
         const int ib = i + S;
+        // Interior pair, wave-uniform: for every record of the wave both
+        // blocks are full ciphertext blocks and neither is the last one (no
+        // AAD, length block, partial block or trailer word), so loads and
+        // stores are unconditional 16-byte accesses and GHASH takes them
+        // unmasked.  Most pairs of a record take this path.
+        if (__all(!valid || (i >= 1 && 16 * ib < ct_len))) {
+          uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+          if (valid && !(gopts() & 17)) {
+            Ca = ld16(rec + 16 * i);
+            Cb = ld16(rec + 16 * ib);
+          }
+          uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
+          if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+          uint4 Ba = Ca, Bb = Cb;
+          if (MODE == 1) {
+            Ba = xor4(Ca, ka);
+            Bb = xor4(Cb, kb);
+          }
+          if (MODE != 2 && valid && !(gopts() & 9)) {
+            st16(orec + 16 * i, MODE == 1 ? Ba : xor4(Ca, ka));
+            st16(orec + 16 * ib, MODE == 1 ? Bb : xor4(Cb, kb));
+          }
+          if (gopts() & 2)
+            Y = xor4(xor4(Y, Ba), Bb);
+          else
+            Y = xor4(gf_mul8(xor4(gf_mul8(Y, lds, gl), Ba), lds, gl), Bb);
+          m += 2;
+          continue;
+        }
         const bool hca = valid && i >= 1 && i <= nct, hcb = valid && ib <= nct;
         uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
         if (hca && !(gopts() & 17)) Ca = ld16(rec + 16 * i);
