@@ -289,6 +289,11 @@ extern "C" {
 
 int espgpu_abi_version(void) { return ESPGPU_ABI_VERSION; }
 
+int espgpu_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : ESPGPU_ENODEV;
+}
+
 const char *espgpu_last_error(espgpu_ctx *c) { return c ? c->err.c_str() : "no context"; }
 
 int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {

@@ -105,6 +105,7 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.espgpu_abi_version.restype = C.c_int
+        L.espgpu_device_count.restype = C.c_int
         L.espgpu_init.argtypes = [C.POINTER(Config), C.POINTER(vp)]
         L.espgpu_fini.argtypes = [vp]
         L.espgpu_fini.restype = None

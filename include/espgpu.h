@@ -152,6 +152,10 @@ typedef struct espgpu_ctx espgpu_ctx;
 /* ---- lifecycle (a kernel-domain shim calls crypto_get_driverid(...,
  *      CRYPTOCAP_F_HARDWARE|CRYPTOCAP_F_SYNC), crypto.c:989, around these) ---- */
 int  espgpu_abi_version(void);
+/* Visible HIP devices (>= 0), or ESPGPU_ENODEV.  One F-Stack process (lcore)
+ * opens one context; process k of a node takes device k mod count
+ * (ff_gpucrypto_host_init_proc). */
+int  espgpu_device_count(void);
 int  espgpu_init(const struct espgpu_config *cfg, espgpu_ctx **out);
 void espgpu_fini(espgpu_ctx *ctx);
 const char *espgpu_last_error(espgpu_ctx *ctx);

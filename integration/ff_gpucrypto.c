@@ -36,7 +36,6 @@
 #include <sys/errno.h>
 #include <sys/kernel.h>
 #include <sys/mbuf.h>
-#include <sys/module.h>
 #include <opencrypto/cryptodev.h>
 #include "cryptodev_if.h"
 #endif
@@ -235,43 +234,74 @@ const struct kmock_cryptodev ff_gpucrypto_kmock = {
 	gpucrypto_newsession, gpucrypto_freesession, gpucrypto_process,
 };
 #else
-static void
-gpucrypto_identify(driver_t *drv, device_t parent)
-{
-	if (device_find_child(parent, "gpucrypto", -1) == NULL &&
-	    BUS_ADD_CHILD(parent, 0, "gpucrypto", 0) == 0)
-		panic("gpucrypto: could not attach");
-}
+/*
+ * F-Stack builds subr_kobj.c but not subr_bus.c (lib/Makefile:323-359), so
+ * there is no newbus to attach a DRIVER_MODULE the way cryptosoft does
+ * (cryptosoft.c:1490-1510).  The driver is a kobj of its own class instead:
+ * crypto.c reaches it only through CRYPTODEV_*(cap->cc_dev, ...) kobj calls
+ * (crypto.c:641,954,980,1730) and device_get_nameunit()/device_printf()
+ * (crypto.c:996,1046,1139), defined here for this one device.  ff_init()
+ * calls ff_gpucrypto_attach() once after ff_freebsd_init() (crypto_init has
+ * run by then); the host domain reaches it through lib/ff_api.symlist.
+ */
+#include <sys/kobj.h>
+#include <machine/stdarg.h>
 
-static int
-gpucrypto_probe(device_t dev)
-{
-	device_set_desc(dev, "MI355X ESP crypto (libespgpu)");
-	return (BUS_PROBE_NOWILDCARD);
-}
-
-static device_method_t gpucrypto_methods[] = {
-	DEVMETHOD(device_identify,	gpucrypto_identify),
-	DEVMETHOD(device_probe,		gpucrypto_probe),
-	DEVMETHOD(device_attach,	gpucrypto_attach),
-	DEVMETHOD(device_detach,	gpucrypto_detach),
-
-	DEVMETHOD(cryptodev_probesession, gpucrypto_probesession),
-	DEVMETHOD(cryptodev_newsession,	gpucrypto_newsession),
-	DEVMETHOD(cryptodev_freesession, gpucrypto_freesession),
-	DEVMETHOD(cryptodev_process,	gpucrypto_process),
-
-	DEVMETHOD_END
+struct _device {
+	KOBJ_FIELDS;
+	const char *nameunit;
 };
 
-static driver_t gpucrypto_driver = {
-	"gpucrypto",
-	gpucrypto_methods,
-	0,
+static kobj_method_t gpucrypto_methods[] = {
+	KOBJMETHOD(cryptodev_probesession, gpucrypto_probesession),
+	KOBJMETHOD(cryptodev_newsession, gpucrypto_newsession),
+	KOBJMETHOD(cryptodev_freesession, gpucrypto_freesession),
+	KOBJMETHOD(cryptodev_process, gpucrypto_process),
+	KOBJMETHOD_END
 };
-static devclass_t gpucrypto_devclass;
+DEFINE_CLASS_0(gpucrypto, gpucrypto_class, gpucrypto_methods, 0);
 
-DRIVER_MODULE(gpucrypto, nexus, gpucrypto_driver, gpucrypto_devclass, 0, 0);
-MODULE_VERSION(gpucrypto, 1);
-MODULE_DEPEND(gpucrypto, crypto, 1, 1, 1);
+static struct _device gpucrypto_dev;
+
+const char *
+device_get_nameunit(device_t dev)
+{
+	return (dev->nameunit);
+}
+
+const char *
+device_get_name(device_t dev)
+{
+	return ("gpucrypto");
+}
+
+int
+device_printf(device_t dev, const char *fmt, ...)
+{
+	va_list ap;
+	int n;
+
+	n = printf("%s: ", dev->nameunit);
+	va_start(ap, fmt);
+	n += vprintf(fmt, ap);
+	va_end(ap);
+	return (n);
+}
+
+int ff_gpucrypto_attach(void);
+int ff_gpucrypto_detach(void);
+
+int
+ff_gpucrypto_attach(void)
+{
+	kobj_init((kobj_t)&gpucrypto_dev, &gpucrypto_class);
+	gpucrypto_dev.nameunit = "gpucrypto0";
+	return (gpucrypto_attach(&gpucrypto_dev));
+}
+
+int
+ff_gpucrypto_detach(void)
+{
+	return (gpucrypto_detach(&gpucrypto_dev));
+}
 #endif

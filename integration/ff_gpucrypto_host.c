@@ -25,6 +25,16 @@ void ff_gpucrypto_done(void *opaque, int etype) __attribute__((weak));
 void ff_gpucrypto_unblock(void) __attribute__((weak));
 
 static espgpu_ctx *g_ctx;          /* one F-Stack process = one lcore = one ctx */
+/* F-Stack runs no crypto_proc thread (its kproc/kthread stubs never start
+ * one, lib/ff_compat.c:156-171), so a request that crypto_dispatch queues on
+ * ERESTART (crypto.c:1450-1459) would never be re-dispatched there.  With
+ * no-queue set, process() makes room instead of answering ERESTART. */
+static int g_noqueue;
+
+void ff_gpucrypto_host_set_noqueue(int on)
+{
+	g_noqueue = on;
+}
 
 int ff_gpucrypto_host_init(int gpu)
 {
@@ -32,6 +42,19 @@ int ff_gpucrypto_host_init(int gpu)
 
 	c.device = gpu;
 	return espgpu_init(&c, &g_ctx);
+}
+
+/* ff_init(): F-Stack process proc_id (one lcore) opens device
+ * proc_id mod (visible devices), the SPI-sharded layout of INTEGRATION.md
+ * section 6 with one process per GPU. */
+int ff_gpucrypto_host_init_proc(int proc_id)
+{
+	int n = espgpu_device_count();
+
+	if (n <= 0)
+		return ESPGPU_ENODEV;
+	g_noqueue = 1;
+	return ff_gpucrypto_host_init(proc_id % n);
 }
 
 /* as ff_gpucrypto_host_init, with explicit staging sizes (batch_records,
@@ -73,7 +96,19 @@ void ff_gpucrypto_host_freesession(int32_t sid)
  * ERESTART and the framework requeues); the driver maps any other code */
 int ff_gpucrypto_host_process(const struct espgpu_req *r, int hint)
 {
-	return g_ctx ? espgpu_process(g_ctx, r, hint) : ESPGPU_ENXIO;
+	int e;
+
+	if (!g_ctx)
+		return ESPGPU_ENXIO;
+	e = espgpu_process(g_ctx, r, hint);
+	if (e == ESPGPU_ERESTART && g_noqueue) {
+		/* wait for the staged batches (their completions go out with the
+		 * next ff_gpucrypto_poll()), then stage this request */
+		e = espgpu_drain(g_ctx);
+		if (e == ESPGPU_OK)
+			e = espgpu_process(g_ctx, r, hint);
+	}
+	return e;
 }
 
 /* main_loop hook: launch the burst's staged records, deliver completions */

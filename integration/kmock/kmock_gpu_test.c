@@ -14,6 +14,7 @@
 
 extern const struct kmock_cryptodev ff_gpucrypto_kmock;
 int  ff_gpucrypto_host_configure(const struct espgpu_config *c);
+void ff_gpucrypto_host_set_noqueue(int on);
 void ff_gpucrypto_host_fini(void);
 int  ff_gpucrypto_poll(void);
 
@@ -126,6 +127,23 @@ int main(void)
 			CHECK(crp[i].crp_etype == 0);
 			CHECK(memcmp(buf[i] + 16, orig[i] + 16, plen_of(i)) == 0);
 		}
+	}
+	/* F-Stack mode (no crypto_proc thread): the same burst with no-queue
+	 * set never reaches the framework as ERESTART */
+	ff_gpucrypto_host_set_noqueue(1);
+	e0 = st->erestarts;
+	memcpy(buf[2], orig[2], sizeof(buf[2]));
+	for (int i = 0; i < NREC; i++)
+		esp_crp(&crp[i], ses, i, 1);
+	run_burst(crp, NREC);
+	CHECK(st->erestarts == e0);
+	for (int i = 0; i < NREC; i++)
+		esp_crp(&crp[i], ses, i, 0);
+	run_burst(crp, NREC);
+	CHECK(st->erestarts == e0);
+	for (int i = 0; i < NREC; i++) {
+		CHECK(crp[i].crp_etype == 0);
+		CHECK(memcmp(buf[i], orig[i], 16 + plen_of(i)) == 0);
 	}
 	kmock_freesession(ses);
 	kmock_detach();

@@ -44,3 +44,61 @@ def test_kernel_driver_on_gpu():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     assert "kmock gpu OK" in r.stdout
+
+
+REF_LIB = "/root/reference/lib"
+
+
+def _makefile_block(text, start, stop="endif"):
+    """The reference Makefile's `start ... stop` block, verbatim."""
+    i = text.index(start)
+    return text[i:text.index("\n" + stop, i) + len(stop) + 1] + "\n"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_LIB), reason="needs the F-Stack tree")
+def test_fstack_patch_applies_and_fixes_the_ipsec_build(tmp_path):
+    """integration/apply_fstack.sh on a copy of the F-Stack files it touches:
+    the patch applies cleanly, the driver and shim land in lib/, and GNU make
+    evaluates the patched FF_IPSEC blocks to the sources the path needs (the
+    unpatched `#aesni.c \\` line empties CRYPTO_SRCS; xform.c
+    needs gmac.c/gfmult.c; FF_IPSEC_GPU adds the driver, shim and include)."""
+    import shutil
+    lib = tmp_path / "lib"
+    lib.mkdir()
+    for f in ("Makefile", "ff_api.symlist", "ff_dpdk_if.c", "ff_init.c"):
+        shutil.copy(os.path.join(REF_LIB, f), lib / f)
+    sh = os.path.join(D, "apply_fstack.sh")
+    subprocess.run(["sh", sh, str(tmp_path), "--dry-run"], check=True, capture_output=True, timeout=60)
+    subprocess.run(["sh", sh, str(tmp_path)], check=True, capture_output=True, timeout=60)
+    assert (lib / "ff_gpucrypto.c").exists() and (lib / "ff_gpucrypto_host.c").exists()
+
+    def evaluate(mk_text, defs):
+        frag = tmp_path / "frag.mk"
+        frag.write_text(mk_text + "\nprint:\n\t@echo CRYPTO=$(strip $(CRYPTO_SRCS))"
+                        "\n\t@echo OPENCRYPTO=$(strip $(OPENCRYPTO_SRCS))"
+                        "\n\t@echo FF=$(strip $(FF_SRCS))\n\t@echo HOST=$(strip $(FF_HOST_SRCS))"
+                        "\n\t@echo CFLAGS=$(strip $(CFLAGS))\n")
+        r = subprocess.run(["make", "-s", "-f", str(frag), "print"] + defs, capture_output=True,
+                           text=True, timeout=60, check=True)
+        return dict(l.split("=", 1) for l in r.stdout.splitlines())
+
+    orig = open(os.path.join(REF_LIB, "Makefile")).read()
+    new = (lib / "Makefile").read_text()
+    before = evaluate(_makefile_block(orig, "ifdef FF_IPSEC\nCRYPTO_SRCS"), ["FF_IPSEC=1"])
+    assert before["CRYPTO"] == ""                         # the reference bug, reproduced
+    blocks = (_makefile_block(new, "ifdef FF_IPSEC\nCRYPTO_SRCS") +
+              _makefile_block(new, "ifdef FF_IPSEC\nOPENCRYPTO_SRCS") +
+              new[new.index("ifdef FF_IPSEC_GPU"):new.index("#\tcryptodev.c")])
+    after = evaluate(blocks, ["FF_IPSEC=1", "FF_IPSEC_GPU=1", "ESPGPU_ROOT=/opt/espgpu"])
+    assert {"rijndael-alg-fst.c", "rijndael-api.c", "sha1.c", "sha256c.c", "sha512c.c"} <= set(after["CRYPTO"].split())
+    assert {"gmac.c", "gfmult.c", "cryptosoft.c", "crypto.c"} <= set(after["OPENCRYPTO"].split())
+    assert after["FF"].split() == ["ff_gpucrypto.c"] and after["HOST"].split() == ["ff_gpucrypto_host.c"]
+    assert "-I/opt/espgpu/include" in after["CFLAGS"] and "-DFF_IPSEC_GPU" in after["CFLAGS"]
+
+    syms = (lib / "ff_api.symlist").read_text().split()
+    assert {"ff_gpucrypto_done", "ff_gpucrypto_unblock", "ff_gpucrypto_attach"} <= set(syms)
+    loop = (lib / "ff_dpdk_if.c").read_text()
+    i = loop.index("process_msg_ring(qconf->proc_id, pkts_burst);")
+    assert loop.index("ff_gpucrypto_poll();", i) < loop.index("lr->loop(lr->arg)", i)
+    init = (lib / "ff_init.c").read_text()
+    assert init.index("ff_freebsd_init();") < init.index("ff_gpucrypto_attach()") < init.index("ff_dpdk_if_up();")
