@@ -759,6 +759,69 @@ int espgpu_drain(espgpu_ctx *c) {
   return 0;
 }
 
+int espgpu_replay_check_batch(espgpu_ctx *c, const uint8_t *d_arena, espgpu_desc *d_desc, uint32_t n,
+                              const espgpu_replay *d_replay, uint32_t nreplay, const uint32_t *d_bitmap,
+                              uint8_t *d_rstatus, void *stream) {
+  if (!c || (n && (!d_arena || !d_desc || !d_rstatus || (nreplay && (!d_replay || !d_bitmap)))))
+    return ESPGPU_EINVAL;
+  if (launch_replay_check(d_arena, d_desc, n, d_replay, nreplay, d_bitmap, d_rstatus, stream))
+    return fail(c, ESPGPU_EIO, "replay check kernel launch failed");
+  return 0;
+}
+
+int espgpu_replay_merge(espgpu_ctx *c, uint8_t *d_status, const uint8_t *d_rstatus, uint32_t n, void *stream) {
+  if (!c || (n && (!d_status || !d_rstatus))) return ESPGPU_EINVAL;
+  if (launch_replay_merge(d_status, d_rstatus, n, stream))
+    return fail(c, ESPGPU_EIO, "replay merge kernel launch failed");
+  return 0;
+}
+
+// ipsec_updatereplay (freebsd/netipsec/ipsec.c:1338-1436) with the window
+// helpers advance_window / set_window (:1203-1232): after authentication, in
+// arrival order per SA.
+int espgpu_replay_update(espgpu_replay *r, uint32_t *bitmap, uint32_t seq) {
+  if (!r || (r->wsize && !bitmap)) return ESPGPU_EINVAL;
+  if (r->wsize == 0) return 0;
+  if (seq == 0 && r->last == 0) return ESPGPU_EACCES;
+  uint32_t *bm = bitmap + r->bitmap_off;
+  const uint32_t mask = r->bitmap_size - 1;
+  auto seen = [&](uint32_t s) { return (bm[(s >> 5) & mask] >> (s & 31)) & 1u; };
+  auto mark = [&](uint32_t s) { bm[(s >> 5) & mask] |= 1u << (s & 31); };
+  auto advance = [&](uint64_t s) {      // clear the words the window top moves past
+    const uint64_t cur = r->last >> 5;
+    uint64_t diff = (s >> 5) - cur;
+    if (diff > r->bitmap_size) diff = r->bitmap_size;
+    for (uint64_t k = 0; k < diff; ++k) bm[(k + cur + 1) & mask] = 0;
+  };
+  const uint32_t window = r->wsize << 3;
+  const uint32_t tl = (uint32_t)r->last, th = (uint32_t)(r->last >> 32);
+  const uint32_t bl = tl - window + 1;
+  if ((tl >= window - 1 && seq >= bl) || (tl < window - 1 && seq < bl)) {
+    if (seq <= tl) {
+      if (seen(seq)) return ESPGPU_EACCES;
+      mark(seq);
+    } else {
+      const uint64_t s = ((uint64_t)th << 32) | seq;
+      advance(s);
+      mark(seq);
+      r->last = s;
+    }
+    return 0;
+  }
+  if (!(r->flags & ESPGPU_REPLAY_ESN)) return ESPGPU_EACCES;
+  if (tl < window - 1 && seq >= bl) {   // in the window, previous subspace
+    if (th == 0 || seen(seq)) return ESPGPU_EACCES;
+    mark(seq);
+    return 0;
+  }
+  if (th + 1 == 0) return ESPGPU_EACCES;   // the high part would wrap
+  const uint64_t s = ((uint64_t)(th + 1) << 32) | seq;
+  advance(s);
+  mark(seq);
+  r->last = s;
+  return 0;
+}
+
 int espgpu_get_stats(espgpu_ctx *c, espgpu_stats *st) {
   if (!c || !st) return ESPGPU_EINVAL;
   *st = c->stats;

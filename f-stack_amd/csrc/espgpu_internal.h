@@ -117,6 +117,9 @@ int set_eta_opts(uint32_t opts);
 // fused: 1 = the one-pass out-of-place decrypt (MODE 0) / verify-first
 // in-place kernel (MODE 2); 0 = verify pass + block-parallel decrypt pass
 int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream);
+int launch_replay_check(const uint8_t *arena, espgpu_desc *desc, uint32_t n, const espgpu_replay *rp,
+                        uint32_t nrp, const uint32_t *bitmap, uint8_t *rstatus, void *stream);
+int launch_replay_merge(uint8_t *status, const uint8_t *rstatus, uint32_t n, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream);

@@ -72,6 +72,15 @@ class Desc(C.Structure):
                 ("esn_hi", C.c_uint32), ("salt", C.c_uint32)]
 
 
+class Replay(C.Structure):
+    """struct espgpu_replay: one SA's replay window (secreplay, keydb.h:206-213)."""
+    _fields_ = [("last", C.c_uint64), ("wsize", C.c_uint32), ("bitmap_size", C.c_uint32),
+                ("bitmap_off", C.c_uint32), ("flags", C.c_uint32)]
+
+
+REPLAY_ESN, REPLAY_CYCSEQ, EACCES = 0x1, 0x2, 13
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("max_sessions", C.c_uint32),
                 ("batch_records", C.c_uint32), ("batch_bytes", C.c_uint32),
@@ -123,6 +132,9 @@ def lib():
         L.espgpu_decrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint32, vp]
         L.espgpu_encrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp]
         L.espgpu_decrypt_batch_trailer.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint32, vp]
+        L.espgpu_replay_check_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp, vp, vp]
+        L.espgpu_replay_merge.argtypes = [vp, vp, vp, C.c_uint32, vp]
+        L.espgpu_replay_update.argtypes = [C.POINTER(Replay), C.POINTER(C.c_uint32), C.c_uint32]
         L.espgpu_last_kernel_ms.argtypes = [vp]
         L.espgpu_last_kernel_ms.restype = C.c_float
         L.espgpu_set_tuning.argtypes = [vp, C.c_char_p, C.c_int]

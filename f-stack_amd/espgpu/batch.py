@@ -70,3 +70,30 @@ def decrypt_host(driver, arena, desc, n, status, out, chunk=0, flags=0):
         out.data_ptr(), chunk, flags)
     if rc:
         raise RuntimeError("espgpu_decrypt_host: %s" % driver.last_error())
+
+
+REPLAY_DTYPE = np.dtype([("last", "<u8"), ("wsize", "<u4"), ("bitmap_size", "<u4"),
+                         ("bitmap_off", "<u4"), ("flags", "<u4")])
+assert REPLAY_DTYPE.itemsize == 24
+
+
+def replay_check(driver, arena, desc, n, replay, bitmap, rstatus, stream=None):
+    """Replay pre-filter (espgpu_replay_check_batch): replay is a uint8 CUDA
+    tensor of REPLAY_DTYPE records indexed by session id, bitmap an int32 CUDA
+    tensor of window words; rstatus receives 0 / EACCES per record, and desc
+    is updated in place (len 0 for replayed records, esn_hi for ESN SAs)."""
+    for t in (arena, desc, replay, bitmap, rstatus):
+        assert t.is_cuda and t.is_contiguous()
+    nrep = replay.numel() // REPLAY_DTYPE.itemsize
+    rc = driver.lib.espgpu_replay_check_batch(
+        driver.ctx, arena.data_ptr(), desc.data_ptr(), n, replay.data_ptr(), nrep,
+        bitmap.data_ptr(), rstatus.data_ptr(), _stream_ptr(stream))
+    if rc:
+        raise RuntimeError("espgpu_replay_check_batch: %s" % driver.last_error())
+
+
+def replay_merge(driver, status, rstatus, n, stream=None):
+    rc = driver.lib.espgpu_replay_merge(driver.ctx, status.data_ptr(), rstatus.data_ptr(), n,
+                                        _stream_ptr(stream))
+    if rc:
+        raise RuntimeError("espgpu_replay_merge: %s" % driver.last_error())

@@ -239,6 +239,41 @@ int  espgpu_decrypt_host(espgpu_ctx *ctx, const uint8_t *h_arena, uint64_t arena
                          const struct espgpu_desc *h_desc, uint32_t n, uint8_t *h_status,
                          uint8_t *h_out, uint32_t chunk, uint32_t flags);
 
+/* ---- replay window (esp_input's pre-crypto check and esp_input_cb's
+ *      update, freebsd/netipsec/xform_esp.c:329-340, :565-580) ----
+ * One SA's window as ipsec_chkreplay reads it (struct secreplay,
+ * netipsec/keydb.h:206-213): `last` = ESN high << 32 | low of the window
+ * top, `wsize` in bytes (window = wsize * 8 packets, 0 = no replay check),
+ * `bitmap_size` u32 words (a power of two, key.c:3346-3351) starting at word
+ * `bitmap_off` of a shared bitmap array. */
+#define ESPGPU_REPLAY_ESN    0x1     /* SADB_X_SAFLAGS_ESN  */
+#define ESPGPU_REPLAY_CYCSEQ 0x2     /* SADB_X_EXT_CYCSEQ   */
+#define ESPGPU_EACCES        13      /* replayed (esp_input's EACCES, esps_replay) */
+struct espgpu_replay {
+	uint64_t last;
+	uint32_t wsize;
+	uint32_t bitmap_size;
+	uint32_t bitmap_off;
+	uint32_t flags;
+};
+
+/* Pre-filter a device-resident batch against the windows as they stand
+ * (ipsec_chkreplay, ipsec.c:1248-1331, for every record in parallel; the
+ * record's SA indexes d_replay[nreplay]): d_rstatus[i] = 0 or ESPGPU_EACCES.
+ * A replayed record's descriptor gets len = 0, so the decrypt kernels drop
+ * it (status EINVAL) without crypto work; an accepted record of an ESN SA
+ * gets esn_hi = the window's high word, as esp_input fills crp_esn.  Run it
+ * before espgpu_decrypt_batch, then espgpu_replay_merge.  Asynchronous. */
+int  espgpu_replay_check_batch(espgpu_ctx *ctx, const uint8_t *d_arena, struct espgpu_desc *d_desc,
+                               uint32_t n, const struct espgpu_replay *d_replay, uint32_t nreplay,
+                               const uint32_t *d_bitmap, uint8_t *d_rstatus, void *stream);
+/* d_status[i] = d_rstatus[i] where that is nonzero. */
+int  espgpu_replay_merge(espgpu_ctx *ctx, uint8_t *d_status, const uint8_t *d_rstatus, uint32_t n,
+                         void *stream);
+/* Host: ipsec_updatereplay (ipsec.c:1338-1436) for one authenticated record,
+ * in arrival order per SA: 0 (window advanced / bit set) or ESPGPU_EACCES. */
+int  espgpu_replay_update(struct espgpu_replay *r, uint32_t *bitmap, uint32_t seq);
+
 /* Device time of the last batch's crypto kernel (ms, from HIP events on the
  * batch stream), for the roofline accounting in bench.py. */
 float espgpu_last_kernel_ms(espgpu_ctx *ctx);

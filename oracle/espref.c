@@ -1276,3 +1276,111 @@ double oref_batch_encrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *o
 {
 	return run_batch(sas, arena, off4, len, sa_idx, esn_hi, NULL, n, nthreads, 1);
 }
+
+/* ---- replay window: freebsd/netipsec/ipsec.c:1177-1436 -------------------
+ * Bit b of the window is bit (b & 31) of word (b >> 5) & (bitmap_size - 1)
+ * (IPSEC_REDUNDANT_BIT_SHIFTS 5, IPSEC_BITMAP_INDEX_MASK, :1177-1180); the
+ * window spans wsize * 8 sequence numbers below and including `last`. */
+static int rp_check_window(const oref_replay *r, uint64_t seq)      /* :1191-1201 */
+{
+	return (r->bitmap[(seq >> 5) & (r->bitmap_size - 1)] >> (seq & 31)) & 1u;
+}
+
+static void rp_advance_window(const oref_replay *r, uint64_t seq)   /* :1203-1221 */
+{
+	uint64_t cur = r->last >> 5, idx = seq >> 5, diff = idx - cur, i;
+	if (diff > r->bitmap_size)
+		diff = r->bitmap_size;
+	for (i = 0; i < diff; i++)
+		r->bitmap[(i + cur + 1) & (r->bitmap_size - 1)] = 0;
+}
+
+static void rp_set_window(const oref_replay *r, uint64_t seq)       /* :1223-1232 */
+{
+	r->bitmap[(seq >> 5) & (r->bitmap_size - 1)] |= 1u << (seq & 31);
+}
+
+int oref_chkreplay(uint32_t seq, uint32_t *seqhigh, oref_replay *r)  /* :1248-1331 */
+{
+	uint32_t window, tl, th, bl;
+	if (r->wsize == 0)
+		return 1;
+	if (seq == 0 && r->last == 0)
+		return 0;
+	window = r->wsize << 3;
+	tl = (uint32_t)r->last;
+	th = (uint32_t)(r->last >> 32);
+	bl = tl - window + 1;
+	if ((tl >= window - 1 && seq >= bl) || (tl < window - 1 && seq < bl)) {
+		*seqhigh = th;
+		if (seq <= tl && rp_check_window(r, seq))
+			return 0;
+		return 1;
+	}
+	if (tl == 0xffffffffu && !(r->flags & OREF_REPLAY_ESN)) {
+		r->overflow++;
+		if (!(r->flags & OREF_REPLAY_CYCSEQ))
+			return 0;
+	}
+	if (tl < window - 1 && seq >= bl) {
+		if (th == 0)
+			return 0;
+		*seqhigh = th - 1;
+		if (rp_check_window(r, seq))
+			return 0;
+		return 1;
+	}
+	*seqhigh = th + 1;
+	if (th + 1 == 0) {
+		r->overflow++;
+		if (!(r->flags & OREF_REPLAY_CYCSEQ))
+			return 0;
+	}
+	return 1;
+}
+
+int oref_updatereplay(uint32_t seq, oref_replay *r)                   /* :1338-1436 */
+{
+	uint32_t window, tl, th, bl, seqh;
+	if (r->wsize == 0)
+		return 0;
+	if (seq == 0 && r->last == 0)
+		return 1;
+	window = r->wsize << 3;
+	tl = (uint32_t)r->last;
+	th = (uint32_t)(r->last >> 32);
+	bl = tl - window + 1;
+	if ((tl >= window - 1 && seq >= bl) || (tl < window - 1 && seq < bl)) {
+		seqh = th;
+		if (seq <= tl) {
+			if (rp_check_window(r, seq))
+				return 1;
+			rp_set_window(r, seq);
+		} else {
+			rp_advance_window(r, ((uint64_t)seqh << 32) | seq);
+			rp_set_window(r, seq);
+			r->last = ((uint64_t)seqh << 32) | seq;
+		}
+		r->count++;
+		return 0;
+	}
+	if (!(r->flags & OREF_REPLAY_ESN))
+		return 1;
+	if (tl < window - 1 && seq >= bl) {
+		if (th == 0)
+			return 1;
+		if (rp_check_window(r, seq))
+			return 1;
+		rp_set_window(r, seq);
+		r->count++;
+		return 0;
+	}
+	seqh = th + 1;
+	if (seqh == 0)
+		return 1;
+	rp_advance_window(r, ((uint64_t)seqh << 32) | seq);
+	rp_set_window(r, seq);
+	r->last = ((uint64_t)seqh << 32) | seq;
+	r->count++;
+	return 0;
+}

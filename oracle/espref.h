@@ -14,6 +14,8 @@
  *   freebsd/opencrypto/cryptosoft.c              swcr_gcm / swcr_eta / swcr_encdec /
  *                                                swcr_authcompute request processing
  *   freebsd/netipsec/xform_esp.c                 esp_input / esp_output request layout
+ *   freebsd/netipsec/ipsec.c                     replay window: ipsec_chkreplay /
+ *                                                ipsec_updatereplay
  *
  * Pinning: primitives are checked against the reference's own
  * rijndael-alg-fst.c / gfmult.c compiled from /root/reference (oracle/_ref),
@@ -107,6 +109,24 @@ double oref_batch_decrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *o
 double oref_batch_encrypt(oref_sa *const *sas, uint8_t *arena, const uint32_t *off4,
                           const uint16_t *len, const uint16_t *sa_idx,
                           const uint32_t *esn_hi, long n, int nthreads);
+
+/* Replay window (struct secreplay, netipsec/keydb.h:206-213), with the SA
+ * flags the checks read: bit 0 SADB_X_SAFLAGS_ESN, bit 1 SADB_X_EXT_CYCSEQ. */
+typedef struct {
+	uint64_t count;
+	uint64_t last;
+	uint32_t wsize;            /* bytes: window = wsize * 8 packets */
+	uint32_t bitmap_size;      /* u32 words, a power of two */
+	uint32_t *bitmap;
+	int overflow;
+	int flags;
+} oref_replay;
+#define OREF_REPLAY_ESN    1
+#define OREF_REPLAY_CYCSEQ 2
+/* ipsec_chkreplay (ipsec.c:1248-1331): 1 permitted (seqhigh set), 0 not. */
+int oref_chkreplay(uint32_t seq, uint32_t *seqhigh, oref_replay *r);
+/* ipsec_updatereplay (ipsec.c:1338-1436): 0 OK (window updated), 1 NG. */
+int oref_updatereplay(uint32_t seq, oref_replay *r);
 
 #ifdef __cplusplus
 }

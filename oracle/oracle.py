@@ -66,8 +66,50 @@ def lib():
         L.oref_batch_encrypt.restype = C.c_double
         L.oref_batch_encrypt.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, u32p, u16p, u16p,
                                          u32p, C.c_long, C.c_int]
+        L.oref_chkreplay.argtypes = [C.c_uint32, u32p, C.c_void_p]
+        L.oref_updatereplay.argtypes = [C.c_uint32, C.c_void_p]
         _lib = L
     return _lib
+
+
+class _ReplayC(C.Structure):
+    _fields_ = [("count", C.c_uint64), ("last", C.c_uint64), ("wsize", C.c_uint32),
+                ("bitmap_size", C.c_uint32), ("bitmap", C.POINTER(C.c_uint32)),
+                ("overflow", C.c_int), ("flags", C.c_int)]
+
+
+REPLAY_ESN, REPLAY_CYCSEQ = 1, 2
+
+
+class Replay:
+    """An SA's replay window (struct secreplay, keydb.h:206-213) driven by the
+    restated ipsec_chkreplay / ipsec_updatereplay (ipsec.c:1248-1436).  The
+    bitmap size follows key_setsaval (key.c:3346-3351): the smallest power of
+    two >= wsize + 4 bytes, in 32-bit words."""
+
+    def __init__(self, wsize, last=0, flags=0):
+        import numpy as np
+        words = 1
+        while wsize + 4 > words:
+            words <<= 1
+        words = max(words // 4, 1)
+        self.bitmap = np.zeros(words, dtype=np.uint32)
+        self.c = _ReplayC(0, last, wsize, words,
+                          self.bitmap.ctypes.data_as(C.POINTER(C.c_uint32)), 0, flags)
+
+    def check(self, seq):
+        """(permitted, seqhigh)"""
+        sh = C.c_uint32(0xFFFFFFFF)
+        ok = lib().oref_chkreplay(seq & 0xFFFFFFFF, C.byref(sh), C.byref(self.c))
+        return bool(ok), sh.value
+
+    def update(self, seq):
+        """True if the window accepted seq (ipsec_updatereplay returned 0)"""
+        return lib().oref_updatereplay(seq & 0xFFFFFFFF, C.byref(self.c)) == 0
+
+    @property
+    def last(self):
+        return self.c.last
 
 
 class SA:

@@ -67,13 +67,14 @@ class EtaSA:
                           self.key + (self.salt if self.ctr else b""), self.akey, esn=self.esn)
 
 
-def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None, tails=None):
+def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None, tails=None, seqs=None):
     """Plaintext ESP records + oracle-encrypted copies in one arena.
 
     Returns (arena_plain, arena_ct, descs, esn_hi) as numpy arrays; records are
     placed at 4-byte aligned offsets (stride_pad adds slack between records).
     tails: {record index: 3 bytes} forced as the payload's last three bytes
-    (last pad byte, pad length, next header).
+    (last pad byte, pad length, next header).  seqs: the records' sequence
+    numbers (default i + 1).
     """
     n = len(sa_idx)
     alens = np.array([sas[s].mlen for s in sa_idx], dtype=np.int64)
@@ -94,7 +95,8 @@ def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None
         rec = arena[o:o + L]
         rec[:] = payload[o:o + L]
         rec[0:4] = np.frombuffer(sa.spi.to_bytes(4, "big"), dtype=np.uint8)
-        rec[4:8] = np.frombuffer(int(i + 1).to_bytes(4, "big"), dtype=np.uint8)
+        sn = int(i + 1) if seqs is None else int(seqs[i])
+        rec[4:8] = np.frombuffer(sn.to_bytes(4, "big"), dtype=np.uint8)
         rec[L - alen:] = 0
         if tails is not None and i in tails:        # last 3 payload bytes
             rec[L - alen - 3:L - alen] = np.frombuffer(bytes(tails[i]), dtype=np.uint8)
