@@ -314,6 +314,10 @@ def profile_traffic(config, inplace, kernel, kern_ms):
                       "avg_kernel_ms": pm.get("avg_kernel_ms")}
     if kernel in dom:
         out["traffic"] = pm.get("hbm_bytes_per_launch")
+        if pm.get("pipes"):
+            # the compute resources of the same kernel: LDS-array and VALU-issue
+            # busy shares and the floor each would set alone (tools/prof_summary.py)
+            out["pipes"] = pm["pipes"]
         if pm.get("avg_kernel_ms"):
             out["profile"]["avg_over_live"] = round(pm["avg_kernel_ms"] / kern_ms, 3)
     else:

@@ -7,6 +7,13 @@ HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced read (16 B/lane loads), so it is doubled; WRITE_SIZE is exact for
 16-B/lane stores.
+
+`pipes` prices the kernel against its compute resources from the same counters
+(per launch; kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs):
+  lds_frac  = SQ_LDS_IDX_ACTIVE / 256 CUs / kernel cycles   (LDS-array busy share)
+  valu_frac = SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / kernel cycles (a wave64 VALU
+              instruction holds its SIMD 2 cycles on gfx950, MI355X_MICROARCH.md:54)
+and the floor each resource alone would set at that clock.
 """
 import collections
 import csv
@@ -48,6 +55,22 @@ def counters(d, sub, match):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def pipes(c, kern_ms):
+    """Busy shares of the LDS array and the VALU issue slots (module docstring)."""
+    cyc = c["GRBM_GUI_ACTIVE"] / 8
+    ghz = cyc / (kern_ms * 1e6)
+    out = {"kernel_cycles": round(cyc), "clock_ghz": round(ghz, 3)}
+    if "SQ_LDS_IDX_ACTIVE" in c:
+        lds = c["SQ_LDS_IDX_ACTIVE"] / 256
+        out.update(lds_cycles_per_cu=round(lds), lds_frac=round(lds / cyc, 3),
+                   lds_floor_ms=round(lds / ghz / 1e6, 4))
+    if "SQ_INSTS_VALU" in c:
+        valu = c["SQ_INSTS_VALU"] * 2 / 1024
+        out.update(valu_cycles_per_simd=round(valu), valu_frac=round(valu / cyc, 3),
+                   valu_floor_ms=round(valu / ghz / 1e6, 4))
+    return out
+
+
 def main():
     argv = [a for a in sys.argv[1:] if a != "--inplace"]
     inplace = "--inplace" in sys.argv
@@ -71,6 +94,7 @@ def main():
         res["hbm_bytes_per_launch"] = rd + wr
     if "GRBM_GUI_ACTIVE" in c:
         res["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / ks[dominant]["avg_ns"]
+        res["pipes"] = pipes(c, steady_ms or ks[dominant]["avg_ns"] / 1e6)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "%s.json" % tag), "w") as f:
         json.dump(res, f, indent=1)
@@ -83,7 +107,8 @@ def main():
                        "avg_kernel_ms": round(steady_ms or ks[dominant]["avg_ns"] / 1e6, 4),
                        "avg_kernel_ms_all_calls": round(ks[dominant]["avg_ns"] / 1e6, 4),
                        "calls": ks[dominant]["calls"],
-                       "hbm_bytes_per_launch": round(res["hbm_bytes_per_launch"])}, f, indent=1)
+                       "hbm_bytes_per_launch": round(res["hbm_bytes_per_launch"]),
+                       "pipes": res.get("pipes")}, f, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
     print("dominant:", dominant, ks[dominant])
 
