@@ -53,8 +53,6 @@ namespace {
 constexpr uint32_t LDS_GT = 0;          // H^S, 256 values x 16 positions x 16 B
 constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
 constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
-constexpr int S = kGcmLanesPerRec;      // lanes per record
-constexpr int RPW = 64 / S;             // records per wave
 
 // Round keys are read through the constant address space: uniform loads from
 // it become s_load (SGPRs, scalar cache) instead of vector loads or LDS reads.
@@ -380,7 +378,7 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
 // Steps m, m+1 of a lane run together: 2 independent AES blocks, then
 // GHASH as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with the 8-bit table.
-template <int MODE>
+template <int MODE, int S>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
                                          uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk) {
   const int lane = threadIdx.x & 63;
@@ -607,8 +605,13 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
-template <int MODE, int WG>
+// S lanes per record: kGcmLanesPerRec for throughput, kGcmLanesSmall for
+// batches too small to fill the chip (half the serial steps per record).
+template <int MODE, int WG, int S>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
+  static_assert(S == kGcmLanesPerRec || S == kGcmLanesSmall, "GHASH tables exist for these strides");
+  constexpr int RPW = 64 / S;             // records per wave
+  constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
 
@@ -621,7 +624,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   }
 
   const bool implicit = (p.chunks == nullptr);
-  const uint32_t nch = implicit ? (p.n + kChunkRecs - 1) / kChunkRecs : *p.nchunks;
+  const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
   uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
   const int wave = tid >> 6;
   // Dynamic chunk queue: chunk costs differ by up to ~300x (64-B vs 9000-B
@@ -637,8 +640,8 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
     if (c >= nch) break;
     uint32_t sa, start, count;
     if (implicit) {
-      start = c * kChunkRecs;
-      count = min((uint32_t)kChunkRecs, p.n - start);
+      start = c * p.chunk;
+      count = min(p.chunk, p.n - start);
       sa = p.desc[start].sa;
     } else {
       const Chunk ch = p.chunks[c];
@@ -656,7 +659,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         mlen = s->mlen;
         mode = s->mode;
         if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
-          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + kGh8Off);
+          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + gh8);
           uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
 #pragma unroll 4
           for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         continue;
       }
-      do_group<MODE>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
+      do_group<MODE, S>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
     }
   }
   // Every workgroup leaves the loop after drawing exactly one ticket >= nch,
@@ -710,18 +713,39 @@ int set_gcm_opts(uint32_t opts) {
 #endif
 }
 
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream) {
+int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
-  // implicit chunks: no more workgroups than chunks (a 32-record burst is one
-  // chunk: one workgroup instead of 256 that only fill LDS and leave)
-  if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + kChunkRecs - 1) / kChunkRecs)));
-  if (encrypt)
-    hipLaunchKernelGGL((gcm_kernel<1, 1024>), dim3(grid), dim3(1024), 0, st, p);
-  else if (two_pass)
-    hipLaunchKernelGGL((gcm_kernel<2, 1024>), dim3(grid), dim3(1024), 0, st, p);
-  else
-    hipLaunchKernelGGL((gcm_kernel<0, 1024>), dim3(grid), dim3(1024), 0, st, p);
+  constexpr int W = kGcmLanesSmall;
+  const bool small = pp.n < kGcmSmallBatch;
+  GcmParams p = pp;
+  // implicit chunks (caller-grouped batch): kChunkRecs records each, or for a
+  // batch of fewer than grid x kChunkRecs records as few as four waves'
+  // records, so that it spreads over up to `grid` CUs instead of queueing on a
+  // few (one wave per workgroup would stage 128 KiB of LDS tables for 8
+  // records and hold every CU, starving a concurrent burst's kernel); no more
+  // workgroups than chunks (a 32-record burst is one workgroup, not 256 that
+  // only fill LDS and leave)
+  // Chunk sizes are powers of two, so every chunk lies inside one aligned run
+  // of kChunkRecs records (the grouping contract, include/espgpu.h).
+  const uint32_t rpw = 64 / (small ? W : kGcmLanesPerRec), per = (pp.n + (uint32_t)grid - 1) / (uint32_t)grid;
+  p.chunk = 4 * rpw;
+  while (p.chunk < per && p.chunk < (uint32_t)kChunkRecs) p.chunk <<= 1;
+  if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + p.chunk - 1) / p.chunk)));
+  if (small) {
+    if (encrypt)
+      hipLaunchKernelGGL((gcm_kernel<1, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
+    else if (two_pass)
+      hipLaunchKernelGGL((gcm_kernel<2, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
+    else
+      hipLaunchKernelGGL((gcm_kernel<0, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
+  } else if (encrypt) {
+    hipLaunchKernelGGL((gcm_kernel<1, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
+  } else if (two_pass) {
+    hipLaunchKernelGGL((gcm_kernel<2, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
+  } else {
+    hipLaunchKernelGGL((gcm_kernel<0, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

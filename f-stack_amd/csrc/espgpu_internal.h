@@ -42,11 +42,16 @@ static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 //                      position p, value v at v*256 + p*16 (value-major, so
 //                      a row's 16 positions sit in the 16 bank quads; staged
 //                      into LDS, the Horner multiplier, esp_gcm.hip gf_mul8).
+// [kGh8SmallOff, +64 KiB) the same for H^8: the Horner multiplier of the
+//                      small-batch kernel (kGcmLanesSmall lanes per record).
 constexpr int kGcmLanesPerRec = 4;                               // GCM kernel: lanes per record
+constexpr int kGcmLanesSmall = 8;                                // small batches: shorter serial chain
+constexpr uint32_t kGcmSmallBatch = 32768;                       // records: below, 8 lanes per record still fit the chip
 constexpr uint32_t kGhPowerBytes = 32 * 16 * 16;                 // 8192
 constexpr uint32_t kGh8Off = 8 * kGhPowerBytes;
 constexpr uint32_t kGh8Bytes = 16 * 256 * 16;                    // 65536
-constexpr uint32_t kGhTableBytes = kGh8Off + kGh8Bytes;          // 131072
+constexpr uint32_t kGh8SmallOff = kGh8Off + kGh8Bytes;
+constexpr uint32_t kGhTableBytes = kGh8SmallOff + kGh8Bytes;     // 196608
 
 // A chunk: up to kChunkRecs records of ONE session, processed by one
 // workgroup iteration of the GCM kernel.  rec positions index `order`
@@ -68,7 +73,7 @@ struct GcmParams {
   const uint32_t *nchunks;        // [0] = GCM (+invalid) chunks, [1] = all chunks
   uint32_t n;                     // number of descriptors (implicit mode)
   const DevSA *sas;
-  const uint8_t *gtab;            // [slot][65536]
+  const uint8_t *gtab;            // [slot][kGhTableBytes]
   const uint2 *tpair;             // 256 x (Te0[x], Te1[x])
   uint8_t *status;
   uint32_t nsas;
@@ -77,6 +82,7 @@ struct GcmParams {
   // Launches sharing a ctx must be stream-ordered (as the planner workspace).
   uint32_t *queue;
   uint32_t *trailer;              // decrypt: fused esp_input_cb trailer words, or nullptr
+  uint32_t chunk;                 // implicit mode: records per chunk (launch_gcm sets it)
 };
 
 struct EtaParams {

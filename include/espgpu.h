@@ -196,7 +196,8 @@ int  espgpu_get_stats(espgpu_ctx *ctx, struct espgpu_stats *st);
  * d_arena: then a verify-first two-pass kernel keeps EBADMSG records intact).
  * encrypt: payload encrypted in place, ICV written.
  * `flags`: ESPGPU_BATCH_GROUPED if d_desc is already grouped by session with
- * at most one session per run of 128 records (skips the device planner).
+ * at most one session per aligned run of 256 records (skips the device
+ * planner; records of another session than their run's come back EINVAL).
  * `stream` is a hipStream_t (NULL = default stream).  Asynchronous.
  * Launches on one ctx are stream-ordered by the library: the work-queue
  * counters and planner workspace belong to the ctx, so a launch on a stream

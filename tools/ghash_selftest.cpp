@@ -1,8 +1,9 @@
 // Host self-test of the GHASH table layouts the GCM kernel uses
 // (host_crypto.cpp ghash_tables): the 8-bit H^S section (LDS, gf_mul8) and
-// the 4-bit H^1..H^8 section (global, gf_mul4_global), each evaluated exactly
-// the way esp_gcm.hip indexes it, against gf128_mul (SP 800-38D Alg. 1).
-// Also the stride-8 Horner + final H^(8-l) combination against a serial
+// the 4-bit H^1..H^8 section (global, gf_mul4_global) and the 8-bit H^8
+// section of the small-batch kernel, each evaluated exactly the way
+// esp_gcm.hip indexes it, against gf128_mul (SP 800-38D Alg. 1).  Also the
+// stride-S Horner + final H^(S-l) combination, S = 4 and 8, against a serial
 // GHASH.  Built and run by tests/test_host_selftests.py.
 #include <cstdio>
 #include <cstdlib>
@@ -11,12 +12,13 @@
 
 // layout constants, mirrored from espgpu_internal.h (which needs HIP vector types)
 static constexpr int S = 4;   // kGcmLanesPerRec: lanes per record = Horner stride
+static constexpr int S2 = 8;  // kGcmLanesSmall: the small-batch kernel's stride
 static constexpr unsigned kGhPowerBytes = 8192, kGh8Off = 8 * 8192, kGh8Bytes = 65536,
-                          kGhTableBytes = kGh8Off + kGh8Bytes;
+                          kGh8SmallOff = kGh8Off + kGh8Bytes, kGhTableBytes = kGh8SmallOff + kGh8Bytes;
 #include "host_crypto.h"
 
 using namespace espgpu;
-static_assert(kGhTableBytes == 131072, "layout");
+static_assert(kGhTableBytes == 196608, "layout");
 
 static void xor16(uint8_t *a, const uint8_t *b) { for (int i = 0; i < 16; ++i) a[i] ^= b[i]; }
 
@@ -48,6 +50,9 @@ int main() {
       for (auto &v : x) v = rand() & 0xff;
       hc::gf128_mul(x, pw[S], a);
       mul8(tabs.data() + kGh8Off, x, b);
+      if (memcmp(a, b, 16)) { printf("8-bit H^S table mismatch\n"); return 1; }
+      hc::gf128_mul(x, pw[S2], a);
+      mul8(tabs.data() + kGh8SmallOff, x, b);
       if (memcmp(a, b, 16)) { printf("8-bit H^8 table mismatch\n"); return 1; }
       for (int e = 1; e <= 8; ++e) {
         hc::gf128_mul(x, pw[e], a);
@@ -56,7 +61,10 @@ int main() {
       }
     }
     // stride-S Horner over N blocks (front-padded to S*M) vs serial GHASH
+    for (int st : {S, S2})
     for (int N : {1, 3, 8, 9, 93, 562}) {
+      const int S = st;
+      const unsigned g8 = S == 4 ? kGh8Off : kGh8SmallOff;
       std::vector<uint8_t> X(16 * N);
       for (auto &v : X) v = rand() & 0xff;
       uint8_t ser[16] = {0}, t[16];
@@ -66,14 +74,14 @@ int main() {
       for (int l = 0; l < S; ++l) {
         uint8_t Y[16] = {0};
         for (int m = 0; m < M; ++m) {
-          if (m > 0) { mul8(tabs.data() + kGh8Off, Y, t); memcpy(Y, t, 16); }
+          if (m > 0) { mul8(tabs.data() + g8, Y, t); memcpy(Y, t, 16); }
           const int i = S * m + l - pad;
           if (i >= 0) xor16(Y, &X[16 * i]);
         }
         mul4(tabs.data() + (S - 1 - l) * kGhPowerBytes, Y, t);
         xor16(Z, t);
       }
-      if (memcmp(Z, ser, 16)) { printf("Horner mismatch N=%d\n", N); return 1; }
+      if (memcmp(Z, ser, 16)) { printf("Horner mismatch S=%d N=%d\n", S, N); return 1; }
     }
   }
   printf("ghash selftest OK\n");
