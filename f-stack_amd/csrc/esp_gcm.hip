@@ -12,7 +12,9 @@
 // Mapping (MI355X-first, not a translation of the 16-byte-at-a-time loop):
 //  * S = kGcmLanesPerRec = 4 lanes per ESP record, 16 records per wave, 16
 //    waves per workgroup, one workgroup per CU (128 KiB LDS); workgroups take
-//    256-record chunks of ONE session from a ticket counter.
+//    256-record chunks of ONE session from a ticket counter.  Batches below
+//    kGcmSmallBatch records run with S = kGcmLanesSmall = 8 (half the serial
+//    steps per record) in smaller chunks spread over the CUs (launch_gcm).
 //  * GHASH is reassociated so every lane runs a Horner chain with the SAME
 //    multiplier H^S over blocks l, l+S, l+2S, ... of its record (the block
 //    list is front-padded with zero blocks to a multiple of S, which leaves
