@@ -410,10 +410,41 @@ def e2e_leg(drv, arena, desc, d, n, pkt_bytes, args, world, dist):
     dt = time.perf_counter() - t0
     dt, all_bytes = aggregate(dist, world, dt, pkt_bytes, arena.device)
     ok = int((h_st != 0).sum()) == 0
-    return {"value": round(all_bytes * reps / dt / 1e9, 2), "unit": "GB/s",
-            "ms_per_batch": round(dt * 1e3 / reps, 3), "chunk_records": args.e2e_chunk,
-            "status_ok": ok,
-            "path": "pinned host -> H2D || kernels || D2H (3 HIP streams) -> pinned host"}
+    res = {"value": round(all_bytes * reps / dt / 1e9, 2), "unit": "GB/s",
+           "ms_per_batch": round(dt * 1e3 / reps, 3), "chunk_records": args.e2e_chunk,
+           "status_ok": ok,
+           "path": "pinned host -> H2D || kernels || D2H (3 HIP streams) -> pinned host"}
+    try:
+        # the ceiling of this leg: the same bytes copied H2D and D2H at once
+        # (two streams, no kernel), as GB/s of packets in each direction
+        bw = pcie_bidir_gbs(src, h_out, arena)
+        res["pcie_bidir_copy_gbs"] = round(bw, 2)
+        res["frac_of_copy"] = round(res["value"] / bw, 3)
+    except Exception as e:                        # informational only
+        log("pcie copy measurement skipped: %s" % e)
+    return res
+
+
+def pcie_bidir_gbs(h_src, h_dst, d_buf, reps=3):
+    """Bytes per second in each direction with an H2D copy of h_src into one
+    half of the device and a D2H copy of the other half into h_dst running
+    concurrently on two streams."""
+    import torch
+    nb = h_src.numel()
+    d_in = torch.empty(nb, dtype=torch.uint8, device=d_buf.device)
+    d_out = torch.empty(nb, dtype=torch.uint8, device=d_buf.device)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        with torch.cuda.stream(s1):
+            d_in.copy_(h_src, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h_dst.copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del d_in, d_out
+    return nb * reps / dt / 1e9
 
 
 def cpu_share():
