@@ -515,3 +515,44 @@ def test_two_streams_one_ctx(drv):
             assert (out.cpu().numpy()[m] == plain[m]).all(), rep
     for s in sids:
         drv.freesession(s)
+
+
+@pytest.mark.parametrize("n", [1, 7, 33, 257, 4097, 32767, 32768, 40000])
+def test_grouped_batch_sizes_across_the_small_batch_path(drv, n):
+    """Caller-grouped batches on both sides of the small-batch switch
+    (kGcmSmallBatch = 32768: 8 lanes per record and power-of-two chunks of
+    32..256 records below it, 4 lanes and 256-record chunks at and above it),
+    decrypted out of place, in place and re-encrypted: statuses and bytes
+    bit-exact vs the oracle, tag failures included."""
+    from espgpu.batch import decrypt_batch, encrypt_batch
+    rng = np.random.default_rng(4000 + n)
+    sas = [GcmSA(rng, 16, esn=True, mlen=16)]
+    sids = _sessions(drv, sas)
+    cts = rng.choice([4, 44, 204, 1448, 2996], n)
+    eh = rng.integers(0, 2**32, n, dtype=np.uint32)
+    plain, ct, descs, eh = build_records(rng, sas, np.zeros(n, dtype=np.int64), cts, esn_hi=eh)
+    descs["sa"] = sids[0]
+    bad = ct.copy()
+    flip = rng.random(n) < 0.05
+    for i in np.nonzero(flip)[0]:
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        bad[o + int(rng.integers(0, L))] ^= 0x02
+    ref_out, ref_st = oracle_decrypt(sas, bad, _oracle_descs(descs), eh)
+    ok_mask = payload_mask(descs[ref_st == 0], len(bad))
+    for inplace in (False, True):
+        arena = _dev(bad)
+        out = arena if inplace else torch.zeros_like(arena)
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        decrypt_batch(drv, arena, _descs_dev(descs), n, st, out=None if inplace else out, grouped=True)
+        torch.cuda.synchronize()
+        got = st.cpu().numpy()
+        assert (got == ref_st).all(), (inplace, np.nonzero(got != ref_st)[0][:10])
+        assert (out.cpu().numpy()[ok_mask] == plain[ok_mask]).all(), inplace
+    arena = _dev(plain)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, _descs_dev(descs), n, st, grouped=True)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert (arena.cpu().numpy() == ct).all()
+    for s in sids:
+        drv.freesession(s)
