@@ -137,18 +137,22 @@ def test_cfg3_1k_eta_sas(drv):
         drv.freesession(int(s))
 
 
-def test_cfg4_rank0_of_8_spi_shard(drv):
+@pytest.mark.parametrize("rank", range(8))
+def test_cfg4_rank_of_8_spi_shard(drv, rank):
+    """cfg4's per-GPU workload for every rank of an 8-GPU job: the rank's
+    ~1K SAs of 8192 random SPIs (fnv1_32(spi) mod 8, key.c:295) and their
+    packets, decrypted through the planner on this one GPU vs the oracle."""
     from espgpu.shard import gpu_of_spi, random_spis, shard_plan
     world, nsa_glob, n_glob = 8, 8192, 8 * 16384
     spis = random_spis(nsa_glob, 0xC4)
     sa_glob = np.random.default_rng(0xC40).integers(0, nsa_glob, n_glob)
-    local_sas, local_pkts = shard_plan(spis, sa_glob, 0, world)
-    assert 900 < len(local_sas) < 1150 and all(gpu_of_spi(spis[i], world) == 0 for i in local_sas)
+    local_sas, local_pkts = shard_plan(spis, sa_glob, rank, world)
+    assert 900 < len(local_sas) < 1150 and all(gpu_of_spi(spis[i], world) == rank for i in local_sas)
     remap = np.full(nsa_glob, -1, dtype=np.int64)
     remap[local_sas] = np.arange(len(local_sas))
     sa_idx = remap[sa_glob[local_pkts]]
     assert (sa_idx >= 0).all()
-    rng = np.random.default_rng(0xC41)
+    rng = np.random.default_rng(0xC41 + rank)
     sas = [GcmSA(rng, 16, spi=int(spis[i])) for i in local_sas]
     sids = _sessions(drv, sas)
     n = len(local_pkts)
