@@ -857,7 +857,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         have = false;                                       // another decrypt launch's session
       } else if (MODE == 4 && (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR)) {
         have = false;                                       // the other cipher's pass
-      } else if (MODE == 3 && !wide_hash(s->aalg)) {
+      } else if (MODE == 3 && !wide_hash(s->aalg) && !p.two_pass_all) {
         have = false;                                       // the fused launches' session
       } else if ((MODE == 5 || MODE == 6) && wide_hash(s->aalg)) {
         have = false;                                       // MODE 3's session
@@ -1125,6 +1125,8 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     // verify-first kernel (in place)
     if (in_place) {
       hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    } else if (p.two_pass_all) {
+      hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else {
       if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);

@@ -98,10 +98,13 @@ struct espgpu_ctx {
   // ETA sessions: all, and by kernel: narrow-hash (SHA-1 / SHA2-256) CBC and
   // CTR, wide-hash (SHA2-384/512) CBC and CTR
   int n_eta = 0, n_cbc = 0, n_ctr = 0, n_wcbc = 0, n_wctr = 0;
-  // ETA decrypt kernels (launch_eta; set_tuning "eta_fused"): 1 = one fused
-  // pass out of place / verify-first kernel in place (cfg3 2.50 / 2.44 ms),
-  // 0 = separate verify and decrypt kernels (2.51 / 2.55 ms)
-  int eta_fused = 1;
+  // ETA decrypt kernels (launch_eta; set_tuning "eta_fused"): 2 (default) =
+  // out of place the verify-first two-pass kernel (MODE 3: HMAC lane = record,
+  // then the block-parallel decrypt of the verified records into out; cfg3
+  // 2.39-2.45 ms), in place MODE 2 (2.44 ms); 1 = out of place one fused pass
+  // per cipher (MODE 0, 2.53-2.55 ms); 0 = separate verify and decrypt
+  // kernels (2.52 / 2.55 ms)
+  int eta_fused = 2;
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -274,7 +277,8 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.nsas = nsas;
     const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wcbc > 0 ? 4 : 0) |
                    (c->n_wctr > 0 ? 8 : 0);
-    if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, c->eta_fused, st))
+    q.two_pass_all = c->eta_fused == 2;
+    if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, c->eta_fused != 0, st))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
@@ -905,7 +909,7 @@ int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_by
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
-  if (!strcmp(key, "eta_fused")) { c->eta_fused = value != 0; return 0; }
+  if (!strcmp(key, "eta_fused")) { c->eta_fused = value < 0 || value > 2 ? 1 : value; return 0; }
   if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
   if (!strcmp(key, "eta_opts")) return set_eta_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
   return ESPGPU_ENOENT;

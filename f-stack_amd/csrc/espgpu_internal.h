@@ -101,6 +101,7 @@ struct EtaParams {
   const uint8_t *isbox;           // inverse S-box (256 B)
   uint8_t *status;
   uint32_t nsas;
+  uint32_t two_pass_all;           // out of place: MODE 3 serves every ETA session (eta_fused 2)
 };
 
 // esp_input_cb's checks on the last 3 plaintext bytes (xform_esp.c:597-630),

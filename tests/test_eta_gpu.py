@@ -215,15 +215,16 @@ def _mask_var(descs, size, hl, ml):
     return m
 
 
-@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("fused", [2, 1, 0])
 @pytest.mark.parametrize("esn", [False, True])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
     """AES-CBC / AES-CTR x HMAC-SHA1-96 / HMAC-SHA2 sessions mixed in one
     batch (planner path), AES-128/192/256, tag failures anywhere in the
     record: statuses and plaintext bit-exact vs the oracle, failed records
-    untouched in place.  fused=0: the separate verify + block-decrypt kernels
-    (set_tuning eta_fused)."""
+    untouched in place.  fused (set_tuning eta_fused): 2 = the default
+    two-pass MODE 3 kernel out of place, 1 = the one-pass fused MODE 0
+    kernels, 0 = the separate verify + block-decrypt kernels."""
     from espgpu.batch import decrypt_batch
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
     rng = np.random.default_rng(1300 + 2 * esn + inplace)
@@ -260,7 +261,7 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
         assert (res[m_bad] == bad[m_bad]).all()
     for s in sids:
         drv.freesession(s)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 1) == 0
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
 
 
 def test_eta_variants_encrypt_vs_oracle(drv):
