@@ -25,8 +25,14 @@
 #ifndef ESPGPU_H
 #define ESPGPU_H
 
+#if defined(_KERNEL) && defined(__FreeBSD__)
+/* F-Stack's kernel domain (lib/Makefile: -nostdinc, FreeBSD headers only):
+ * the driver ff_gpucrypto.c includes this header for the request mirrors */
+#include <sys/types.h>
+#else
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -24,6 +24,12 @@
  * Completions come back on the lcore thread from ff_gpucrypto_poll() (host
  * domain, main_loop) through ff_gpucrypto_done() below.
  *
+ * Built two ways: with the FreeBSD headers in F-Stack's kernel domain, where
+ * it is a DRIVER_MODULE on lib/ff_newbus.c's nexus0
+ * (tests/test_fstack_build.py compiles and link-checks that build), and with
+ * -DFF_GPUCRYPTO_KMOCK against integration/kmock, a test double of the
+ * crypto KPI that the CPU and GPU tests drive.
+ *
  * Errors cross the boundary as libespgpu's ABI codes (include/espgpu.h) and
  * are translated to FreeBSD kernel errno here, in gpucrypto_errno().
  */
@@ -36,6 +42,7 @@
 #include <sys/errno.h>
 #include <sys/kernel.h>
 #include <sys/mbuf.h>
+#include <sys/module.h>
 #include <opencrypto/cryptodev.h>
 #include "cryptodev_if.h"
 #endif
@@ -59,6 +66,8 @@ void ff_gpucrypto_done(void *opaque, int abi_etype);
 void ff_gpucrypto_unblock(void);
 
 static int32_t gpucrypto_id = -1;
+
+int gpucrypto_errno(int abi);
 
 /* libespgpu ABI code -> FreeBSD errno (sys/errno.h) */
 int
@@ -235,73 +244,58 @@ const struct kmock_cryptodev ff_gpucrypto_kmock = {
 };
 #else
 /*
- * F-Stack builds subr_kobj.c but not subr_bus.c (lib/Makefile:323-359), so
- * there is no newbus to attach a DRIVER_MODULE the way cryptosoft does
- * (cryptosoft.c:1490-1510).  The driver is a kobj of its own class instead:
- * crypto.c reaches it only through CRYPTODEV_*(cap->cc_dev, ...) kobj calls
- * (crypto.c:641,954,980,1730) and device_get_nameunit()/device_printf()
- * (crypto.c:996,1046,1139), defined here for this one device.  ff_init()
- * calls ff_gpucrypto_attach() once after ff_freebsd_init() (crypto_init has
- * run by then); the host domain reaches it through lib/ff_api.symlist.
+ * In F-Stack: a newbus driver on nexus0 (lib/ff_newbus.c), attached like
+ * cryptosoft (cryptosoft.c:1443-1510) when mi_startup loads the
+ * DRIVER_MODULEs, after cryptosoft's own module has run crypto_init
+ * (SI_ORDER_ANY sorts after DRIVER_MODULE's SI_ORDER_MIDDLE).  ff_init()
+ * opens the GPU context before ff_freebsd_init() (ff_gpucrypto_host_init_proc);
+ * without one the probe declines and cryptosoft keeps every session.
  */
-#include <sys/kobj.h>
-#include <machine/stdarg.h>
+#include "bus_if.h"
+#include "device_if.h"
 
-struct _device {
-	KOBJ_FIELDS;
-	const char *nameunit;
+int ff_gpucrypto_host_ready(void);
+
+static void
+gpucrypto_identify(driver_t *drv, device_t parent)
+{
+	(void)drv;
+	if (device_find_child(parent, "gpucrypto", -1) == NULL)
+		BUS_ADD_CHILD(parent, 0, "gpucrypto", 0);
+}
+
+static int
+gpucrypto_probe(device_t dev)
+{
+	if (!ff_gpucrypto_host_ready())
+		return (ENXIO);
+	device_set_desc(dev, "MI355X ESP bulk crypto (libespgpu)");
+	return (BUS_PROBE_NOWILDCARD);
+}
+
+static device_method_t gpucrypto_methods[] = {
+	DEVMETHOD(device_identify,	gpucrypto_identify),
+	DEVMETHOD(device_probe,		gpucrypto_probe),
+	DEVMETHOD(device_attach,	gpucrypto_attach),
+	DEVMETHOD(device_detach,	gpucrypto_detach),
+
+	DEVMETHOD(cryptodev_probesession, gpucrypto_probesession),
+	DEVMETHOD(cryptodev_newsession,	gpucrypto_newsession),
+	DEVMETHOD(cryptodev_freesession, gpucrypto_freesession),
+	DEVMETHOD(cryptodev_process,	gpucrypto_process),
+
+	DEVMETHOD_END
 };
 
-static kobj_method_t gpucrypto_methods[] = {
-	KOBJMETHOD(cryptodev_probesession, gpucrypto_probesession),
-	KOBJMETHOD(cryptodev_newsession, gpucrypto_newsession),
-	KOBJMETHOD(cryptodev_freesession, gpucrypto_freesession),
-	KOBJMETHOD(cryptodev_process, gpucrypto_process),
-	KOBJMETHOD_END
+static driver_t gpucrypto_driver = {
+	"gpucrypto",
+	gpucrypto_methods,
+	0,		/* no softc */
 };
-DEFINE_CLASS_0(gpucrypto, gpucrypto_class, gpucrypto_methods, 0);
+static devclass_t gpucrypto_devclass;
 
-static struct _device gpucrypto_dev;
-
-const char *
-device_get_nameunit(device_t dev)
-{
-	return (dev->nameunit);
-}
-
-const char *
-device_get_name(device_t dev)
-{
-	return ("gpucrypto");
-}
-
-int
-device_printf(device_t dev, const char *fmt, ...)
-{
-	va_list ap;
-	int n;
-
-	n = printf("%s: ", dev->nameunit);
-	va_start(ap, fmt);
-	n += vprintf(fmt, ap);
-	va_end(ap);
-	return (n);
-}
-
-int ff_gpucrypto_attach(void);
-int ff_gpucrypto_detach(void);
-
-int
-ff_gpucrypto_attach(void)
-{
-	kobj_init((kobj_t)&gpucrypto_dev, &gpucrypto_class);
-	gpucrypto_dev.nameunit = "gpucrypto0";
-	return (gpucrypto_attach(&gpucrypto_dev));
-}
-
-int
-ff_gpucrypto_detach(void)
-{
-	return (gpucrypto_detach(&gpucrypto_dev));
-}
+EARLY_DRIVER_MODULE_ORDERED(gpucrypto, nexus, gpucrypto_driver, gpucrypto_devclass,
+    NULL, NULL, SI_ORDER_ANY, BUS_PASS_DEFAULT);
+MODULE_VERSION(gpucrypto, 1);
+MODULE_DEPEND(gpucrypto, crypto, 1, 1, 1);
 #endif

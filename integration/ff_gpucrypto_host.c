@@ -65,6 +65,12 @@ int ff_gpucrypto_host_configure(const struct espgpu_config *c)
 	return espgpu_init(c, &g_ctx);
 }
 
+/* the kernel-domain driver's device_probe: attach only with a GPU context */
+int ff_gpucrypto_host_ready(void)
+{
+	return g_ctx != NULL;
+}
+
 void ff_gpucrypto_host_fini(void)
 {
 	if (g_ctx) {

@@ -65,7 +65,8 @@ def test_fstack_patch_applies_and_fixes_the_ipsec_build(tmp_path):
     import shutil
     lib = tmp_path / "lib"
     lib.mkdir()
-    for f in ("Makefile", "ff_api.symlist", "ff_dpdk_if.c", "ff_init.c"):
+    for f in ("Makefile", "ff_api.symlist", "ff_dpdk_if.c", "ff_init.c", "ff_compat.c", "ff_glue.c",
+              "ff_host_interface.c", "ff_host_interface.h"):
         shutil.copy(os.path.join(REF_LIB, f), lib / f)
     sh = os.path.join(D, "apply_fstack.sh")
     subprocess.run(["sh", sh, str(tmp_path), "--dry-run"], check=True, capture_output=True, timeout=60)
@@ -96,9 +97,12 @@ def test_fstack_patch_applies_and_fixes_the_ipsec_build(tmp_path):
     assert "-I/opt/espgpu/include" in after["CFLAGS"] and "-DFF_IPSEC_GPU" in after["CFLAGS"]
 
     syms = (lib / "ff_api.symlist").read_text().split()
-    assert {"ff_gpucrypto_done", "ff_gpucrypto_unblock", "ff_gpucrypto_attach"} <= set(syms)
+    assert {"ff_gpucrypto_done", "ff_gpucrypto_unblock"} <= set(syms)
     loop = (lib / "ff_dpdk_if.c").read_text()
     i = loop.index("process_msg_ring(qconf->proc_id, pkts_burst);")
     assert loop.index("ff_gpucrypto_poll();", i) < loop.index("lr->loop(lr->arg)", i)
     init = (lib / "ff_init.c").read_text()
-    assert init.index("ff_freebsd_init();") < init.index("ff_gpucrypto_attach()") < init.index("ff_dpdk_if_up();")
+    # the GPU context exists before ff_freebsd_init() attaches the drivers
+    assert (init.index("ret = ff_dpdk_init(") < init.index("ff_gpucrypto_host_init_proc(ff_global_cfg")
+            < init.index("ret = ff_freebsd_init();"))
+    assert (lib / "ff_newbus.c").exists()
