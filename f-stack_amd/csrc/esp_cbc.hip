@@ -19,11 +19,12 @@
 //    record's SHA-1 / SHA-256 compressions from the precomputed ipad/opad
 //    chaining states (hmac_init_pad, crypto.c:413-441), rounds fully
 //    unrolled in registers, no tables.
-//  * Out-of-place decrypt (MODE 0, the benchmarked path) is ONE pass per
-//    record (eta_decrypt_fused): every 64-byte HMAC chunk the lane loads also
-//    completes up to four cipher blocks, which it decrypts with four AES
-//    states in flight (aes_dec4 for CBC, aes_enc4 of the counters for CTR)
-//    and stores, so the record is read once.
+//  * Decrypt is verify-first: an HMAC pass (lane = record), then a
+//    block-parallel decrypt of the verified records (MODE 3 out of place, the
+//    default and benchmarked path; MODE 2 in place).  MODE 0 (set_tuning
+//    eta_fused = 1) is the one-pass alternative: every 64-byte HMAC chunk the
+//    lane loads also completes up to four cipher blocks, which it decrypts
+//    with four AES states in flight and stores, so the record is read once.
 //  * In-place verify-first decrypt (MODE 2) must authenticate before it may
 //    overwrite: HMAC pass first, then a block-parallel pass -- the wave walks
 //    its records as one flat block list, 64 consecutive blocks per pass
@@ -785,11 +786,14 @@ __device__ __forceinline__ void fill_pair(uint8_t *lds, uint32_t base, const uin
   }
 }
 
-// MODE 0: decrypt out-of-place (fused, SHA-1 / SHA2-256 sessions of one cipher);
-// 1: encrypt in place; 2: decrypt in place (verify first); 3: decrypt out of
-// place for the SHA2-384/512 sessions (verify pass, then the block-parallel
-// pass of MODE 2 writing to p.out: 128-byte hash blocks do not line up with
-// MODE 0's four-block chunks)
+// MODE 0: decrypt out-of-place, one fused pass (SHA-1 / SHA2-256 sessions of
+// one cipher; used only with set_tuning eta_fused = 1); 1: encrypt in place,
+// MAC pass; 2: decrypt in place (verify first); 3: decrypt out of place,
+// verify pass then the block-parallel pass of MODE 2 writing to p.out -- with
+// p.two_pass_all (eta_fused = 2, the default) for every ETA session, else only
+// for the SHA2-384/512 sessions (128-byte hash blocks do not line up with
+// MODE 0's four-block chunks); 4: encrypt, cipher pass; 5 / 6: the separate
+// decrypt / verify kernels (eta_fused = 0)
 // CKS: MODE 0 is built once per cipher (CK_CBC / CK_CTR) and each launch
 // serves only its cipher's sessions -- both fused paths inlined in one kernel
 // made the register allocator spill; -1 = every ETA session.
@@ -1121,8 +1125,9 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
     hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   } else if (fused) {
-    // round-1/2 layout: one fused pass per cipher (out of place) or the
-    // verify-first kernel (in place)
+    // in place: the verify-first kernel (MODE 2); out of place: MODE 3 for
+    // every session (eta_fused = 2, the default), or the one-pass MODE 0
+    // kernel per cipher plus MODE 3 for SHA2-384/512 (eta_fused = 1)
     if (in_place) {
       hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else if (p.two_pass_all) {

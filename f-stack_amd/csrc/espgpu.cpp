@@ -517,6 +517,9 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
   for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
+  // and the ctx's last launch on any stream: a device-resident batch on the
+  // caller's stream may still be reading this slot's keys
+  if (c->launched) hipEventSynchronize(c->ev_last);
   const Session &fs = c->sessions[sid];
   if (fs.mode == ESPGPU_CSP_MODE_ETA) {
     c->n_eta--;
@@ -763,6 +766,13 @@ int espgpu_drain(espgpu_ctx *c) {
   return 0;
 }
 
+int espgpu_replay_params_ok(const espgpu_replay *r) {
+  if (!r) return 0;
+  if (r->wsize == 0) return 1;
+  const uint32_t b = r->bitmap_size;
+  return b != 0 && (b & (b - 1)) == 0 && (uint64_t)b * 32 >= (uint64_t)r->wsize * 8;
+}
+
 int espgpu_replay_check_batch(espgpu_ctx *c, const uint8_t *d_arena, espgpu_desc *d_desc, uint32_t n,
                               const espgpu_replay *d_replay, uint32_t nreplay, const uint32_t *d_bitmap,
                               uint8_t *d_rstatus, void *stream) {
@@ -786,6 +796,9 @@ int espgpu_replay_merge(espgpu_ctx *c, uint8_t *d_status, const uint8_t *d_rstat
 int espgpu_replay_update(espgpu_replay *r, uint32_t *bitmap, uint32_t seq) {
   if (!r || (r->wsize && !bitmap)) return ESPGPU_EINVAL;
   if (r->wsize == 0) return 0;
+  // the window indexes the bitmap with bitmap_size - 1 as a mask: a power of
+  // two covering wsize * 8 bits (key.c:3346-3351 sizes it so)
+  if (!espgpu_replay_params_ok(r)) return ESPGPU_EINVAL;
   if (seq == 0 && r->last == 0) return ESPGPU_EACCES;
   uint32_t *bm = bitmap + r->bitmap_off;
   const uint32_t mask = r->bitmap_size - 1;
@@ -909,7 +922,11 @@ int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_by
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
-  if (!strcmp(key, "eta_fused")) { c->eta_fused = value < 0 || value > 2 ? 1 : value; return 0; }
+  if (!strcmp(key, "eta_fused")) {
+    if (value < 0 || value > 2) return ESPGPU_EINVAL;
+    c->eta_fused = value;
+    return 0;
+  }
   if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
   if (!strcmp(key, "eta_opts")) return set_eta_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;
   return ESPGPU_ENOENT;

@@ -135,6 +135,7 @@ def lib():
         L.espgpu_replay_check_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp, vp, vp]
         L.espgpu_replay_merge.argtypes = [vp, vp, vp, C.c_uint32, vp]
         L.espgpu_replay_update.argtypes = [C.POINTER(Replay), C.POINTER(C.c_uint32), C.c_uint32]
+        L.espgpu_replay_params_ok.argtypes = [C.POINTER(Replay)]
         L.espgpu_last_kernel_ms.argtypes = [vp]
         L.espgpu_last_kernel_ms.restype = C.c_float
         L.espgpu_set_tuning.argtypes = [vp, C.c_char_p, C.c_int]

@@ -264,6 +264,12 @@ struct espgpu_replay {
 	uint32_t flags;
 };
 
+/* 1 if r's window parameters are usable: wsize 0 (no check), or bitmap_size
+ * a power of two with bitmap_size * 32 >= wsize * 8 bits; else 0.  Both the
+ * batch check and espgpu_replay_update index the bitmap with
+ * bitmap_size - 1 as a mask: the caller of espgpu_replay_check_batch must
+ * pass only windows this accepts (espgpu_replay_update returns EINVAL). */
+int  espgpu_replay_params_ok(const struct espgpu_replay *r);
 /* Pre-filter a device-resident batch against the windows as they stand
  * (ipsec_chkreplay, ipsec.c:1248-1331, for every record in parallel; the
  * record's SA indexes d_replay[nreplay]): d_rstatus[i] = 0 or ESPGPU_EACCES.
@@ -285,8 +291,15 @@ int  espgpu_replay_update(struct espgpu_replay *r, uint32_t *bitmap, uint32_t se
  * batch stream), for the roofline accounting in bench.py. */
 float espgpu_last_kernel_ms(espgpu_ctx *ctx);
 
-/* Tuning knob (engine-internal, for A/B measurement): "grid" (workgroups
- * per launch, 0 = 256, one per CU).  Returns 0 or ENOENT. */
+/* Tuning knobs (engine-internal, for A/B measurement):
+ *   "grid"      workgroups per launch (0 = 256, one per CU);
+ *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
+ *               decrypt (MODE 3) out of place, 1 one fused pass per record
+ *               (MODE 0), 0 separate verify / decrypt kernels; others EINVAL;
+ *   "gcm_opts" / "eta_opts" measurement knobs that skip work on purpose
+ *               (results wrong): only in libespgpu_knobs.so, ENOTSUP in the
+ *               product library unless 0.
+ * Returns 0, EINVAL, ENOTSUP or ENOENT (unknown key). */
 int  espgpu_set_tuning(espgpu_ctx *ctx, const char *key, int value);
 
 #ifdef __cplusplus

@@ -225,8 +225,22 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
     untouched in place.  fused (set_tuning eta_fused): 2 = the default
     two-pass MODE 3 kernel out of place, 1 = the one-pass fused MODE 0
     kernels, 0 = the separate verify + block-decrypt kernels."""
-    from espgpu.batch import decrypt_batch
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
+    try:
+        _eta_variants_decrypt(drv, esn, inplace)
+    finally:
+        # the shared ctx goes back to the default kernels even when this fails
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+
+
+def test_eta_fused_knob_range(drv):
+    for v in (-1, 3, 7):
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == 22
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+
+
+def _eta_variants_decrypt(drv, esn, inplace):
+    from espgpu.batch import decrypt_batch
     rng = np.random.default_rng(1300 + 2 * esn + inplace)
     sas = _variant_sas(rng, esn)
     sids = _sessions(drv, sas)
@@ -261,7 +275,6 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
         assert (res[m_bad] == bad[m_bad]).all()
     for s in sids:
         drv.freesession(s)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
 
 
 def test_eta_variants_encrypt_vs_oracle(drv):

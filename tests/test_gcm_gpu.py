@@ -309,6 +309,39 @@ def test_full_size_roundtrip_1m_x_1500(drv):
     drv.freesession(sids[0])
 
 
+def test_freesession_waits_for_batch_on_user_stream(drv):
+    """espgpu_freesession zeroes the session's device keys: a device-resident
+    batch still running on the caller's own stream must finish under the old
+    keys first (the ctx's last-launch event), so every record verifies."""
+    from espgpu.batch import decrypt_batch, encrypt_batch
+    rng = np.random.default_rng(4242)
+    sas = [GcmSA(rng, 16)]
+    sids = _sessions(drv, sas)
+    n, rec = 1 << 20, 1480
+    g = torch.Generator(device="cuda").manual_seed(11)
+    arena = torch.randint(0, 256, (n * 1500 + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    d = np.zeros(n, dtype=[("off4", "<u4"), ("len", "<u2"), ("sa", "<u2"), ("esn_hi", "<u4"), ("salt", "<u4")])
+    d["off4"] = (np.arange(n, dtype=np.int64) * 1500 + 20) // 4
+    d["len"] = rec
+    d["sa"] = sids[0]
+    d["salt"] = int.from_bytes(sas[0].salt, "little")
+    desc = _descs_dev(d)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, desc, n, st, grouped=True)
+    torch.cuda.synchronize()
+    user = torch.cuda.Stream()
+    out = torch.zeros_like(arena)
+    st.fill_(0xEE)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(user):
+        for _ in range(4):          # several ms of work queued behind the free
+            decrypt_batch(drv, arena, desc, n, st, out=out, grouped=True, stream=user)
+    drv.freesession(sids[0])        # host returns only after the batches ran
+    assert user.query()
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+
+
 @pytest.mark.parametrize("chunk", [0, 97, 1000])
 def test_host_pipeline_vs_oracle(drv, chunk):
     """espgpu_decrypt_host: pinned host records -> chunked H2D/kernel/D2H on

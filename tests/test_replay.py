@@ -89,6 +89,30 @@ def test_host_update_matches_oracle(wsize, flags, last):
     assert (bitmap[:3] == 0xDEADBEEF).all()
 
 
+@pytest.mark.parametrize("wsize,bsize,ok", [
+    (0, 0, True),          # no replay check: the bitmap is never read
+    (8, 0, False),         # no bitmap words
+    (8, 3, False),         # not a power of two: bitmap_size - 1 is no mask
+    (8, 1, False),         # 64 window bits in one 32-bit word
+    (8, 2, True), (8, 4, True),
+    (128, 16, False), (128, 32, True),
+])
+def test_replay_update_rejects_unusable_windows(wsize, bsize, ok):
+    """espgpu_replay_update indexes the bitmap with bitmap_size - 1 as a
+    mask: a window whose bitmap is empty, not a power of two or smaller than
+    wsize * 8 bits is EINVAL, not an out-of-bounds read or write."""
+    from espgpu._lib import Replay
+    L = _lib()
+    rp = Replay(100, wsize, bsize, 0, 0)
+    assert L.espgpu_replay_params_ok(C.byref(rp)) == int(ok)
+    bitmap = np.full(max(bsize, 1) + 4, 0xA5A5A5A5, dtype=np.uint32)
+    got = L.espgpu_replay_update(C.byref(rp), bitmap.ctypes.data_as(C.POINTER(C.c_uint32)), 101)
+    if ok:
+        assert got == 0
+    else:
+        assert got == 22 and rp.last == 100 and (bitmap == 0xA5A5A5A5).all()
+
+
 # ---------------------------------------------------------------- GPU ------
 
 def _torch():
