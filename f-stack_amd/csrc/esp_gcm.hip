@@ -715,11 +715,11 @@ int set_gcm_opts(uint32_t opts) {
 #endif
 }
 
-int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, void *stream) {
+int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   constexpr int W = kGcmLanesSmall;
-  const bool small = pp.n < kGcmSmallBatch;
+  const bool small = lanes ? lanes == W : pp.n < kGcmSmallBatch;
   GcmParams p = pp;
   // implicit chunks (caller-grouped batch): kChunkRecs records each, or for a
   // batch of fewer than grid x kChunkRecs records as few as four waves'

@@ -105,6 +105,9 @@ struct espgpu_ctx {
   // per cipher (MODE 0, 2.53-2.55 ms); 0 = separate verify and decrypt
   // kernels (2.52 / 2.55 ms)
   int eta_fused = 2;
+  // GCM lanes per record: 0 = by batch size, 4 or 8 forced (set_tuning
+  // "gcm_lanes": the tests run both kernels at every batch size)
+  int gcm_lanes = 0;
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -256,7 +259,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, st))
+  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, c->gcm_lanes, st))
     return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if ((kinds & 2) && c->n_eta > 0) {
     EtaParams q{};
@@ -925,6 +928,11 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!strcmp(key, "eta_fused")) {
     if (value < 0 || value > 2) return ESPGPU_EINVAL;
     c->eta_fused = value;
+    return 0;
+  }
+  if (!strcmp(key, "gcm_lanes")) {
+    if (value != 0 && value != kGcmLanesPerRec && value != kGcmLanesSmall) return ESPGPU_EINVAL;
+    c->gcm_lanes = value;
     return 0;
   }
   if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;

@@ -117,7 +117,9 @@ __host__ __device__ inline uint32_t esp_trailer_word(uint32_t wlast, uint32_t pl
 }
 
 // Launchers (defined in the .hip files, called by espgpu.cpp).
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, void *stream);
+// lanes: 0 = by batch size (kGcmLanesSmall below kGcmSmallBatch records,
+// else kGcmLanesPerRec), or force 4 / 8 (set_tuning "gcm_lanes", tests)
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int lanes, void *stream);
 int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
 int set_eta_opts(uint32_t opts);
 // kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones

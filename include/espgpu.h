@@ -293,6 +293,8 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
 
 /* Tuning knobs (engine-internal, for A/B measurement):
  *   "grid"      workgroups per launch (0 = 256, one per CU);
+ *   "gcm_lanes" GCM lanes per record: 0 (default) 8 below 32768 records,
+ *               else 4; 4 or 8 forces one kernel; others EINVAL;
  *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
  *               decrypt (MODE 3) out of place, 1 one fused pass per record
  *               (MODE 0), 0 separate verify / decrypt kernels; others EINVAL;

@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "f-stack_amd"), os.path.join(ROOT, "oracle"), ROOT):
     if p not in sys.path:
@@ -31,3 +33,15 @@ def pytest_configure(config):
     if os.path.isdir("/root/reference/freebsd"):
         _make(["-C", "oracle", "ref"], fatal=False)
     _make(["-C", "f-stack_amd", "-j8"])
+
+
+@pytest.fixture(params=[4, 8], ids=["lanes4", "lanes8"])
+def gcm_lanes(request, drv):
+    """Run a GCM test through both kernels whatever its batch size: 4 lanes
+    per record (the throughput kernel) and 8 (the small-batch kernel, half
+    the serial steps); set_tuning "gcm_lanes", reset afterwards."""
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", request.param) == 0
+    try:
+        yield request.param
+    finally:
+        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", 0)

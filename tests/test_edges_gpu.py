@@ -92,7 +92,7 @@ def _run(drv, sas, ct_lens, rng, inplace, tamper=(1,)):
 
 
 @pytest.mark.parametrize("inplace", [False, True])
-def test_gcm_max_length_records(drv, inplace):
+def test_gcm_max_length_records(drv, inplace, gcm_lanes):
     rng = np.random.default_rng(4100 + inplace)
     sas = [GcmSA(rng, 16), GcmSA(rng, 32, esn=True)]
     ct = MAXLEN - 32                                             # SPI|SN|IV8 + 16-byte ICV

@@ -47,7 +47,7 @@ def _cts(rng, sas, idx):
 
 
 @pytest.mark.parametrize("seed", [11, 12, 13, 14])
-def test_every_session_kind_mixed_vs_oracle(drv, seed):
+def test_every_session_kind_mixed_vs_oracle(drv, seed, gcm_lanes):
     from espgpu.batch import decrypt_batch
     from espgpu.esp import trailer_word
     rng = np.random.default_rng(9000 + seed)

@@ -141,7 +141,7 @@ def _sessions(drv, sas):
 
 @pytest.mark.parametrize("klen", [16, 24, 32])
 @pytest.mark.parametrize("esn", [False, True])
-def test_batch_decrypt_vs_oracle(drv, klen, esn):
+def test_batch_decrypt_vs_oracle(drv, klen, esn, gcm_lanes):
     from espgpu.batch import decrypt_batch
     rng = np.random.default_rng(100 + klen + esn)
     sas = [GcmSA(rng, klen, esn=esn)]
@@ -177,7 +177,7 @@ def _oracle_descs(descs):
     return d
 
 
-def test_batch_encrypt_vs_oracle(drv):
+def test_batch_encrypt_vs_oracle(drv, gcm_lanes):
     from espgpu.batch import encrypt_batch
     rng = np.random.default_rng(9)
     sas = [GcmSA(rng, 16), GcmSA(rng, 32, esn=True)]
@@ -199,7 +199,7 @@ def test_batch_encrypt_vs_oracle(drv):
         drv.freesession(s)
 
 
-def test_batch_inplace_verify_first(drv):
+def test_batch_inplace_verify_first(drv, gcm_lanes):
     """d_out == d_arena: EBADMSG records keep their ciphertext (esp_input_cb contract)."""
     from espgpu.batch import decrypt_batch
     rng = np.random.default_rng(21)
@@ -225,7 +225,7 @@ def test_batch_inplace_verify_first(drv):
     drv.freesession(sids[0])
 
 
-def test_planner_many_sessions_mixed_sizes(drv):
+def test_planner_many_sessions_mixed_sizes(drv, gcm_lanes):
     """Random SA per record (the cfg2 shape, scaled down): device planner path."""
     from espgpu.batch import decrypt_batch
     rng = np.random.default_rng(33)
@@ -342,6 +342,62 @@ def test_freesession_waits_for_batch_on_user_stream(drv):
     assert int((st != 0).sum()) == 0
 
 
+@pytest.mark.parametrize("inplace", [False, True])
+def test_every_line_alignment_vs_oracle(drv, gcm_lanes, inplace):
+    """Every payload alignment (all 32 four-byte offsets in a 128-byte line,
+    out of place also with the output at another alignment than the input),
+    payloads that end anywhere in a 16-byte block or a line, cross the
+    counter-256 run, and the three ICV lengths: decrypt and encrypt bit-exact
+    vs the oracle, trailer words included, through both GCM kernels."""
+    from espgpu.batch import decrypt_batch, encrypt_batch
+    rng = np.random.default_rng(9000 + gcm_lanes + 2 * inplace)
+    sas = [GcmSA(rng, 16), GcmSA(rng, 32, esn=True), GcmSA(rng, 16, mlen=12), GcmSA(rng, 24, mlen=8)]
+    sids = _sessions(drv, sas)
+    cts = [4, 8, 12, 16, 20, 60, 64, 108, 112, 124, 128, 132, 236, 240, 252, 256, 260, 1448, 4092, 4100, 8948]
+    n = 32 * len(cts)
+    sa_idx = rng.integers(0, len(sas), n)
+    ct_l = np.array([cts[i % len(cts)] for i in range(n)])
+    # one record per (alignment, size): stride_pad rotates the start offsets
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, ct_l, stride_pad=4,
+                                         esn_hi=rng.integers(0, 2**32, n, dtype=np.uint32))
+    offs = descs["off4"].astype(np.int64) * 4 + 16
+    assert len(set((offs % 128).tolist())) == 32
+    bad = ct.copy()
+    flip = rng.random(n) < 0.1
+    for i in np.nonzero(flip)[0]:
+        bad[int(descs["off4"][i]) * 4 + int(rng.integers(0, int(descs["len"][i])))] ^= 0x08
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    for shift in ((0,) if inplace else (0, 4, 68)):
+        arena = _dev(bad)
+        obuf = torch.zeros(len(bad) + 128, dtype=torch.uint8, device="cuda")
+        out = arena if inplace else obuf[shift:shift + len(bad)]
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        tr = torch.zeros(n, dtype=torch.int32, device="cuda")
+        decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out, trailer=tr)
+        torch.cuda.synchronize()
+        got = st.cpu().numpy()
+        assert (got == ref_st).all(), (shift, np.nonzero(got != ref_st)[0][:10])
+        alens = np.array([sas[s].mlen for s in sa_idx])
+        m = payload_mask(descs[got == 0], len(bad), 16, alens[got == 0])
+        assert (out.cpu().numpy()[m] == ref_out[m]).all(), shift
+        from espgpu.esp import trailer_word
+        trw = tr.cpu().numpy().view(np.uint32)
+        for i in np.nonzero(got == 0)[0][:200]:
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert trw[i] == trailer_word(bytes(ref_out[o + 16:o + L - int(alens[i])])), i
+        assert (trw[got != 0] == 0).all()
+    arena = _dev(plain)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, _descs_dev(d), n, st)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert (arena.cpu().numpy() == ct).all()
+    for s in sids:
+        drv.freesession(s)
+
+
 @pytest.mark.parametrize("chunk", [0, 97, 1000])
 def test_host_pipeline_vs_oracle(drv, chunk):
     """espgpu_decrypt_host: pinned host records -> chunked H2D/kernel/D2H on
@@ -377,7 +433,7 @@ def test_host_pipeline_vs_oracle(drv, chunk):
 
 
 @pytest.mark.parametrize("grid", [0, 7, 300])
-def test_kernel_grids_vs_oracle(drv, grid):
+def test_kernel_grids_vs_oracle(drv, grid, gcm_lanes):
     """The GCM kernel decrypts (out of place and verify-first in place),
     verifies and encrypts bit-exactly at the default and at odd grid sizes
     (work-queue drain with fewer and more workgroups than CUs), for
@@ -430,7 +486,7 @@ def test_kernel_grids_vs_oracle(drv, grid):
 # bytes of the tag and compares that many, swcr_gcm :598-600, :636)
 
 @pytest.mark.parametrize("mlen", [12, 8])
-def test_truncated_icv_batch_vs_oracle(drv, mlen):
+def test_truncated_icv_batch_vs_oracle(drv, mlen, gcm_lanes):
     """Decrypt (out of place and verify-first in place) and encrypt with
     truncated-ICV sessions mixed with a full-ICV one through the planner."""
     from espgpu.batch import decrypt_batch, encrypt_batch

@@ -69,7 +69,7 @@ def _sessions(drv, sas):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["gcm", "eta"])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_fused_trailer_vs_oracle(drv, kind, inplace):
+def test_fused_trailer_vs_oracle(drv, kind, inplace, gcm_lanes):
     from espgpu.batch import decrypt_batch
     from espgpu.esp import trailer_word
     rng = np.random.default_rng(17 + inplace + 2 * (kind == "eta"))
