@@ -558,6 +558,13 @@ __device__ void hmac_wide(const uint8_t *rec, uint32_t L0, bool esn, uint32_t es
 __device__ __forceinline__ bool wide_hash(uint32_t aalg) {
   return aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || aalg == ESPGPU_CRYPTO_SHA2_512_HMAC;
 }
+// Sessions only the two-pass kernels (MODE 3 / MODE 2) serve: SHA2-384/512
+// (128-byte hash blocks), no auth (CSP_MODE_CIPHER: aalg 0) and ESP-NULL
+// (the identity cipher).  The one-pass MODE 0 and the split MODE 6 / 5
+// kernels take SHA-1 / SHA2-256 with AES-CBC / AES-CTR only.
+__device__ __forceinline__ bool two_pass_only(uint32_t calg, uint32_t aalg) {
+  return wide_hash(aalg) || aalg == 0 || calg == ESPGPU_CRYPTO_NULL_CBC;
+}
 
 __device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
 
@@ -857,25 +864,30 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           p.status[di] = ESPGPU_EINVAL;
           if (MODE != 1 && p.trailer) p.trailer[di] = 0;
         }
-      } else if (MODE == 0 && ((s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR) || wide_hash(s->aalg))) {
+      } else if (MODE == 0 && ((s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR) ||
+                               two_pass_only(s->calg, s->aalg))) {
         have = false;                                       // another decrypt launch's session
-      } else if (MODE == 4 && (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR)) {
-        have = false;                                       // the other cipher's pass
-      } else if (MODE == 3 && !wide_hash(s->aalg) && !p.two_pass_all) {
+      } else if (MODE == 4 && (s->calg == ESPGPU_CRYPTO_NULL_CBC ||
+                               (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR))) {
+        have = false;                                       // the other cipher's pass / no cipher
+      } else if (MODE == 3 && !two_pass_only(s->calg, s->aalg) && !p.two_pass_all) {
         have = false;                                       // the fused launches' session
-      } else if ((MODE == 5 || MODE == 6) && wide_hash(s->aalg)) {
+      } else if ((MODE == 5 || MODE == 6) && two_pass_only(s->calg, s->aalg)) {
         have = false;                                       // MODE 3's session
       } else {
-        const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;
+        const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM, null = s->calg == ESPGPU_CRYPTO_NULL_CBC;
         const uint32_t mlen = s->mlen;
-        hl = ctr ? 16u : 24u;                               // SPI|SN|IV8 or SPI|SN|IV16
-        const int pl = (int)len - (int)hl - (int)mlen;      // alen = mlen
+        hl = ctr ? 16u : null ? 8u : 24u;                   // SPI|SN|IV8, SPI|SN, SPI|SN|IV16
+        const int pl = (int)len - (int)hl - (int)mlen;      // alen = mlen (0: no auth)
         // xform_esp.c:316-324: payload > 0 and a multiple of the cipher's
-        // blocksize (16 for CBC, 1 for CTR; records are 4-byte multiples)
-        valid = pl > 0 && (ctr || (pl & 15) == 0) && (len & 3) == 0;
+        // blocksize (16 for CBC, 1 for CTR, 4 for NULL; records are 4-byte
+        // multiples)
+        valid = pl > 0 && (ctr || null || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
         if (valid && MODE == 5) ok = p.status[di] == ESPGPU_OK;   // verified by the MODE 6 pass
-        if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
+        if (valid && (MODE == 2 || MODE == 3) && s->aalg == 0) {
+          ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
+        } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
           if (MODE == 6) {              // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
@@ -948,7 +960,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
     if (MODE == 1) {
       // ---- encrypt, MAC pass (after MODE 4 wrote the ciphertext): HMAC over
       // SPI|SN|IV|CT (|ESN), ICV = its first mlen bytes ----
-      if (have && valid) {
+      if (have && valid && p.sas[sa].aalg != 0) {           // CSP_MODE_CIPHER: no ICV
         const DevSA *s = p.sas + sa;
         uint8_t *rec = p.arena + off;
         uint32_t dg[16];
@@ -1012,6 +1024,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       run = run && !mine;
       const DevSA *s = p.sas + sau;
       const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;      // wave-uniform
+      const bool null = s->calg == ESPGPU_CRYPTO_NULL_CBC;    // ESP-NULL: the identity
       const uint32_t nb = mine ? (plen + 15) / 16 : 0;
       uint32_t incl = nb;
 #pragma unroll
@@ -1056,7 +1069,9 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           v[k] = pv[k] = make_uint4(0, 0, 0, 0);
           if (fk[k] >= 0) {
             const uint8_t *rec = p.arena + rok[k];
-            if (ctr) {
+            if (null) {
+              v[k] = ld16(rec + 8 + 16 * ik[k]);                                     // P_i = C_i
+            } else if (ctr) {
               pv[k] = ld16(rec + 16 + 16 * ik[k]);                                   // C_i
               v[k] = make_uint4(rsk[k], *reinterpret_cast<const uint32_t *>(rec + 8),
                                 *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(ik[k] + 1));
@@ -1066,10 +1081,12 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
             }
           }
         }
-        if (ctr)
+        if (null) {
+        } else if (ctr) {
           aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
-        else
+        } else {
           aes_dec4(v, kp(s->dk), nr, lds, slot);
+        }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
           if (fk[k] >= 0) {
@@ -1077,10 +1094,13 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
             const uint32_t i = ik[k], rpl = rplk[k];
             const int rem = (int)rpl - 16 * (int)i;
             const uint4 pt = xor4(v[k], pv[k]);
-            if (ctr)
+            if (null) {
+              if (MODE != 2 && p.out != p.arena) st_partial(dst + 8 + 16 * i, pt, rem);   // in place: as is
+            } else if (ctr) {
               st_partial(dst + 16 + 16 * i, pt, rem);
-            else
+            } else {
               st16(dst + 24 + 16 * i, pt);
+            }
             if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdik[k]] = esp_trailer_word(last_word(pt, rem), rpl);
           }
         }

@@ -33,8 +33,10 @@ constexpr uint32_t kSmallBatchBytes = 128u << 10;
 struct Session {
   bool used = false;
   int mode = 0, flags = 0, mlen = 0, klen = 0;
-  bool ctr = false;       // ETA with AES-ICM (RFC 3686 ESP AES-CTR)
-  bool wide = false;      // ETA with HMAC-SHA2-384/512 (128-byte hash blocks)
+  bool ctr = false;       // ETA / CIPHER with AES-ICM (RFC 3686 ESP AES-CTR)
+  bool null = false;      // ETA / CIPHER with CRYPTO_NULL_CBC (ESP-NULL)
+  bool wide = false;      // served by the two-pass ETA kernels only: HMAC-SHA2-384/512
+                          // (128-byte hash blocks), no auth (CIPHER) or ESP-NULL
 };
 
 struct Pending {
@@ -155,6 +157,14 @@ uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) 
 uint32_t be32(const uint8_t *p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
 uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
 uint32_t ror16(uint32_t v) { return (v >> 16) | (v << 16); }
+
+// The ETA-kernel session counter a session belongs to: which decrypt and
+// cipher-pass kernels a batch may need (launch_eta kinds).  ESP-NULL sessions
+// need no cipher pass; they count as CTR so that no CBC pass is launched.
+int &eta_count(espgpu_ctx *c, const Session &s) {
+  const bool ctr = s.ctr || s.null;
+  return s.wide ? (ctr ? c->n_wctr : c->n_wcbc) : (ctr ? c->n_ctr : c->n_cbc);
+}
 
 int ensure_plan(espgpu_ctx *c, uint32_t n) {
   const uint32_t need_chunks = plan_max_chunks(n, c->cfg.max_sessions);
@@ -405,18 +415,36 @@ int espgpu_probesession(const espgpu_session_params *csp) {
       if (csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_NIST_GCM_16 || !aes_klen) return ESPGPU_EINVAL;
       if (csp->csp_ivlen != 12) return ESPGPU_EINVAL;                 // cryptosoft.c:1093
       if (csp->csp_auth_alg != 0 || csp->csp_auth_klen != 0) return ESPGPU_EINVAL;
-      // ICVs of 8/12/16 bytes (RFC 4106 s3.3); the kernels move whole dwords,
-      // so other truncations are left to cryptosoft (probe ESPGPU_EINVAL)
-      if (csp->csp_auth_mlen > 16 || (csp->csp_auth_mlen & 3)) return ESPGPU_EINVAL;
+      // ICVs of 8/12/16 bytes (RFC 4106 s3.3; 0 = 16); other truncations,
+      // which ESP never sets up, are left to cryptosoft (probe ESPGPU_EINVAL)
+      if (csp->csp_auth_mlen != 0 && csp->csp_auth_mlen != 8 && csp->csp_auth_mlen != 12 &&
+          csp->csp_auth_mlen != 16)
+        return ESPGPU_EINVAL;
       if (csp->csp_flags & ESPGPU_CSP_F_ESN) return ESPGPU_EINVAL;    // ESN for GCM = SEPARATE_AAD
+      return ESPGPU_PROBE_HARDWARE;
+    case ESPGPU_CSP_MODE_CIPHER:
+      // ESP with encryption and no auth (esp_init :230-231): AES-CBC or
+      // AES-ICM (csp_ivlen = the enc_xform's 16), or ESP-NULL (no key, no
+      // IV: swcr_null); swcr_probesession :1257-1266 / swcr_cipher_supported
+      // :1228-1239.  No auth fields; esp_init sets no flags for it.
+      if (csp->csp_auth_alg != 0 || csp->csp_auth_klen != 0 || csp->csp_auth_mlen != 0) return ESPGPU_EINVAL;
+      if (csp->csp_flags) return ESPGPU_EINVAL;
+      if (csp->csp_cipher_alg == ESPGPU_CRYPTO_NULL_CBC) return csp->csp_cipher_klen == 0 ? ESPGPU_PROBE_HARDWARE : ESPGPU_EINVAL;
+      if ((csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC && csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_ICM) ||
+          !aes_klen || csp->csp_ivlen != 16)
+        return ESPGPU_EINVAL;
       return ESPGPU_PROBE_HARDWARE;
     case ESPGPU_CSP_MODE_ETA: {
       // AES-CBC or AES-ICM (CTR; csp_ivlen = the enc_xform's 16, the nonce
-      // rides in crp_iv) with HMAC-SHA1 or HMAC-SHA2-256 (esp_init :225-241)
-      if ((csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC && csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_ICM) ||
-          !aes_klen)
+      // rides in crp_iv), or ESP-NULL (CRYPTO_NULL_CBC: no key; cryptosoft
+      // degrades the session to the digest, cryptosoft.c:1394-1398), with
+      // HMAC-SHA1 or HMAC-SHA2-256/384/512 (esp_init :225-241)
+      if (csp->csp_cipher_alg == ESPGPU_CRYPTO_NULL_CBC) {
+        if (csp->csp_cipher_klen != 0) return ESPGPU_EINVAL;
+      } else if ((csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_CBC && csp->csp_cipher_alg != ESPGPU_CRYPTO_AES_ICM) ||
+                 !aes_klen || csp->csp_ivlen != 16) {
         return ESPGPU_EINVAL;
-      if (csp->csp_ivlen != 16) return ESPGPU_EINVAL;
+      }
       int hashlen = 0;
       switch (csp->csp_auth_alg) {                                 // xform_sha1.c, xform_sha2.c
         case ESPGPU_CRYPTO_SHA1_HMAC: hashlen = 20; break;
@@ -438,7 +466,9 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   if (!c || !csp || !sid_out) return ESPGPU_EINVAL;
   int pr = espgpu_probesession(csp);
   if (pr >= 0) return fail(c, ESPGPU_EINVAL, "session parameters not supported");
-  if (!csp->csp_cipher_key) return fail(c, ESPGPU_EINVAL, "per-request keys are not supported; session key required");
+  const bool null_cipher = csp->csp_cipher_alg == ESPGPU_CRYPTO_NULL_CBC;
+  if (!csp->csp_cipher_key && !null_cipher)
+    return fail(c, ESPGPU_EINVAL, "per-request keys are not supported; session key required");
   int slot = -1;
   for (size_t i = 0; i < c->sessions.size(); ++i)
     if (!c->sessions[i].used) { slot = (int)i; break; }
@@ -452,9 +482,10 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   memset(&sa, 0, sizeof sa);
   const uint8_t *key = (const uint8_t *)csp->csp_cipher_key;
   uint32_t rk[60];
-  const int nr = hc::aes_expand_enc(key, csp->csp_cipher_klen, rk);
+  const int nr = null_cipher ? 0 : hc::aes_expand_enc(key, csp->csp_cipher_klen, rk);
   sa.nr = (uint32_t)nr;
-  sa.mode = (uint32_t)csp->csp_mode;
+  // CSP_MODE_CIPHER sessions run in the ETA kernels (aalg 0: no MAC pass)
+  sa.mode = (uint32_t)(csp->csp_mode == ESPGPU_CSP_MODE_CIPHER ? ESPGPU_CSP_MODE_ETA : csp->csp_mode);
   sa.flags = (uint32_t)csp->csp_flags;
   if (csp->csp_mode == ESPGPU_CSP_MODE_AEAD) {
     sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : 16;
@@ -468,21 +499,26 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     hc::ghash_tables(h, kGcmLanesPerRec, tabs.data());
     HIPCHK(c, hipMemcpy(c->d_gtab + (size_t)slot * kGhTableBytes, tabs.data(), kGhTableBytes, hipMemcpyHostToDevice));
   } else {
-    const int aalg = csp->csp_auth_alg;
+    const bool auth = csp->csp_mode == ESPGPU_CSP_MODE_ETA;
+    const int aalg = auth ? csp->csp_auth_alg : 0;
     const bool sha256 = aalg == ESPGPU_CRYPTO_SHA2_256_HMAC;
     const bool wide = aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || aalg == ESPGPU_CRYPTO_SHA2_512_HMAC;
     sa.calg = (uint32_t)csp->csp_cipher_alg;
     sa.aalg = (uint32_t)aalg;
-    // mlen 0 = the whole hash (swcr_setup_auth, cryptosoft.c:1013-1018)
+    // mlen 0 = the whole hash (swcr_setup_auth, cryptosoft.c:1013-1018); no
+    // ICV without auth
     const uint32_t hashlen = sha256 ? 32u : aalg == ESPGPU_CRYPTO_SHA2_384_HMAC ? 48u
                            : aalg == ESPGPU_CRYPTO_SHA2_512_HMAC ? 64u : 20u;
-    sa.mlen = csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : hashlen;
-    for (int i = 0; i < 4 * (nr + 1); ++i) sa.rk[i] = rk[i];
-    uint32_t dk[60];
-    hc::aes_expand_dec(key, csp->csp_cipher_klen, dk);
-    for (int i = 0; i < 4 * (nr + 1); ++i) sa.dk[i] = dk[i];
+    sa.mlen = !auth ? 0u : csp->csp_auth_mlen ? (uint32_t)csp->csp_auth_mlen : hashlen;
+    if (!null_cipher) {
+      for (int i = 0; i < 4 * (nr + 1); ++i) sa.rk[i] = rk[i];
+      uint32_t dk[60];
+      hc::aes_expand_dec(key, csp->csp_cipher_klen, dk);
+      for (int i = 0; i < 4 * (nr + 1); ++i) sa.dk[i] = dk[i];
+    }
     const uint8_t *ak = (const uint8_t *)csp->csp_auth_key;
-    if (wide) {
+    if (!auth) {
+    } else if (wide) {
       const bool is384 = aalg == ESPGPU_CRYPTO_SHA2_384_HMAC;
       hc::hmac_sha512_pad_state(ak, csp->csp_auth_klen, 0x36, is384, sa.ipad);
       hc::hmac_sha512_pad_state(ak, csp->csp_auth_klen, 0x5c, is384, sa.opad);
@@ -493,9 +529,6 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
       hc::hmac_sha1_pad_state(ak, csp->csp_auth_klen, 0x36, sa.ipad);
       hc::hmac_sha1_pad_state(ak, csp->csp_auth_klen, 0x5c, sa.opad);
     }
-    c->n_eta++;
-    const bool ctr = csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
-    (wide ? (ctr ? c->n_wctr : c->n_wcbc) : (ctr ? c->n_ctr : c->n_cbc))++;
   }
   HIPCHK(c, hipMemcpy(c->d_sas + slot, &sa, sizeof sa, hipMemcpyHostToDevice));
   Session &s = c->sessions[slot];
@@ -504,9 +537,15 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   s.flags = csp->csp_flags;
   s.mlen = (int)sa.mlen;
   s.klen = csp->csp_cipher_klen;
-  s.ctr = csp->csp_mode == ESPGPU_CSP_MODE_ETA && csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
-  s.wide = csp->csp_mode == ESPGPU_CSP_MODE_ETA &&
-           (csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_384_HMAC || csp->csp_auth_alg == ESPGPU_CRYPTO_SHA2_512_HMAC);
+  const bool eta_kind = csp->csp_mode != ESPGPU_CSP_MODE_AEAD;
+  s.ctr = eta_kind && csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
+  s.null = eta_kind && null_cipher;
+  s.wide = eta_kind && (sa.aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || sa.aalg == ESPGPU_CRYPTO_SHA2_512_HMAC ||
+                        sa.aalg == 0 || null_cipher);
+  if (eta_kind) {
+    c->n_eta++;
+    eta_count(c, s)++;
+  }
   c->h_sas[slot] = sa;
   *sid_out = slot;
   return 0;
@@ -524,9 +563,9 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   // caller's stream may still be reading this slot's keys
   if (c->launched) hipEventSynchronize(c->ev_last);
   const Session &fs = c->sessions[sid];
-  if (fs.mode == ESPGPU_CSP_MODE_ETA) {
+  if (fs.mode != ESPGPU_CSP_MODE_AEAD) {
     c->n_eta--;
-    (fs.wide ? (fs.ctr ? c->n_wctr : c->n_wcbc) : (fs.ctr ? c->n_ctr : c->n_cbc))--;
+    eta_count(c, fs)--;
   }
   c->sessions[sid] = Session();
   DevSA z;
@@ -558,14 +597,21 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   const Session &ses = c->sessions[sid];
   size_t total = 0;
   for (int i = 0; i < r->nsegs; ++i) total += r->segs[i].len;
-  const bool gcm = ses.mode == ESPGPU_CSP_MODE_AEAD;
+  const bool gcm = ses.mode == ESPGPU_CSP_MODE_AEAD, cipher_only = ses.mode == ESPGPU_CSP_MODE_CIPHER;
   // ICV bytes in the record: the session's (possibly truncated) mlen, 16/12/8
-  // for GCM (cryptosoft.c:1112-1117), 12 or 20 for HMAC-SHA1, 16 for HMAC-SHA2-256-128
-  const int ivlen = (gcm || ses.ctr) ? 8 : 16, hlen = 8 + ivlen, alen = ses.mlen;
+  // for GCM (cryptosoft.c:1112-1117), 12 or 20 for HMAC-SHA1, 16 for
+  // HMAC-SHA2-256-128, none without auth.  IV: 8 for GCM / CTR, none for
+  // ESP-NULL (ivsize 0), else 16.
+  const int ivlen = (gcm || ses.ctr) ? 8 : ses.null ? 0 : 16, hlen = 8 + ivlen, alen = ses.mlen;
   const int plen = r->crp_payload_length;
-  int aad_start = r->crp_aad_start;
+  int aad_start = cipher_only ? r->crp_payload_start - hlen : r->crp_aad_start;
   // ESP shape checks
-  if (plen <= 0 || r->crp_payload_start < 0 || (size_t)(r->crp_digest_start + alen) > total) return reject(ESPGPU_EINVAL);
+  if (plen <= 0 || r->crp_payload_start < hlen ||
+      (size_t)(r->crp_payload_start + plen + alen) > total ||
+      (alen && (size_t)(r->crp_digest_start + alen) > total))
+    return reject(ESPGPU_EINVAL);
+  if (cipher_only && (r->crp_aad || r->crp_aad_length != 0 || (r->crp_op & ESPGPU_CRYPTO_OP_VERIFY_DIGEST)))
+    return reject(ESPGPU_EINVAL);
   uint8_t hdr[8];
   uint32_t esn_hi = 0, salt = 0;
   if (gcm) {
@@ -587,8 +633,9 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
     // AES-CTR: crp_iv = nonce || explicit IV || be32(1) (xform_esp.c:453-458),
     // and the explicit IV is the record's; the kernel rebuilds the counter
     // blocks from the descriptor's salt (the nonce) and the record
-    if (!(r->crp_flags & ESPGPU_CRYPTO_F_IV_SEPARATE) || r->crp_aad || r->crp_aad_length != hlen ||
-        r->crp_payload_start != aad_start + hlen || be32(r->crp_iv + 12) != 1u)
+    if (!(r->crp_flags & ESPGPU_CRYPTO_F_IV_SEPARATE) || r->crp_aad ||
+        (!cipher_only && r->crp_aad_length != hlen) || r->crp_payload_start != aad_start + hlen ||
+        be32(r->crp_iv + 12) != 1u)
       return reject(ESPGPU_EINVAL);
     uint8_t ivb[8];
     if (!seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)(aad_start + 8), 8, ivb) ||
@@ -596,13 +643,20 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
       return reject(ESPGPU_EINVAL);
     salt = le32(r->crp_iv);
     if (ses.flags & ESPGPU_CSP_F_ESN) esn_hi = be32(r->crp_esn);
+  } else if (ses.null) {
+    // ESP-NULL: no IV (crp_iv_start unset, xform_esp.c:459-461), payload a
+    // multiple of the null blocksize 4 (:316-324)
+    if (r->crp_aad || (!cipher_only && r->crp_aad_length != hlen) || r->crp_payload_start != aad_start + hlen ||
+        (plen & 3))
+      return reject(ESPGPU_EINVAL);
+    if (ses.flags & ESPGPU_CSP_F_ESN) esn_hi = be32(r->crp_esn);
   } else {
-    if (r->crp_aad || r->crp_aad_length != hlen || r->crp_iv_start != aad_start + 8 ||
+    if (r->crp_aad || (!cipher_only && r->crp_aad_length != hlen) || r->crp_iv_start != aad_start + 8 ||
         r->crp_payload_start != aad_start + hlen || (plen & 15))
       return reject(ESPGPU_EINVAL);
     if (ses.flags & ESPGPU_CSP_F_ESN) esn_hi = be32(r->crp_esn);
   }
-  if (r->crp_digest_start != r->crp_payload_start + plen) return reject(ESPGPU_EINVAL);
+  if (alen && r->crp_digest_start != r->crp_payload_start + plen) return reject(ESPGPU_EINVAL);
   const uint32_t rlen = (uint32_t)(hlen + plen + alen);
   if (rlen > 65535 || (rlen & 3)) return reject(ESPGPU_EINVAL);
   if (s->nrec >= c->cfg.batch_records || s->bytes + rlen + 16 > c->cfg.batch_bytes) {
@@ -644,7 +698,7 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   // results: payload (+ digest when encrypting) go back to the request buffer
   pd.nspan = 1;
   pd.span[0] = {(uint32_t)r->crp_payload_start, (uint32_t)hlen, (uint32_t)plen};
-  if (op == 1) {
+  if (op == 1 && alen) {
     pd.nspan = 2;
     pd.span[1] = {(uint32_t)r->crp_digest_start, (uint32_t)(hlen + plen), (uint32_t)ses.mlen};
   }

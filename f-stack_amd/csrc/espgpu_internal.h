@@ -15,7 +15,9 @@ namespace espgpu {
 // ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
 //   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
 //   = SHA-1 chaining state after one block of key^0x36 / key^0x5c
-//   (hmac_init_pad, crypto.c:413-441).
+//   (hmac_init_pad, crypto.c:413-441).  CSP_MODE_CIPHER sessions are ETA
+//   sessions to the kernels (mode ETA) with aalg 0 and mlen 0: the cipher pass
+//   alone; calg ESPGPU_CRYPTO_NULL_CBC is the identity cipher (no key, no IV).
 struct DevSA {
   uint32_t rk[64];
   uint32_t dk[64];
@@ -26,8 +28,8 @@ struct DevSA {
   uint32_t ipad[16]; // ETA: HMAC chaining states after the ipad / opad key
   uint32_t opad[16]; //      block (5 words SHA-1, 8 SHA2-256, 16 SHA2-384/512:
                      //      64-bit state word k as words 2k (high), 2k+1)
-  uint32_t calg;    // ETA cipher: ESPGPU_CRYPTO_AES_CBC or _AES_ICM (CTR)
-  uint32_t aalg;    // ETA auth: ESPGPU_CRYPTO_SHA1_HMAC or _SHA2_256/384/512_HMAC
+  uint32_t calg;    // ETA cipher: ESPGPU_CRYPTO_AES_CBC, _AES_ICM (CTR) or _NULL_CBC
+  uint32_t aalg;    // ETA auth: ESPGPU_CRYPTO_SHA1_HMAC or _SHA2_256/384/512_HMAC, 0 = none
   uint32_t pad_[256 - 128 - 4 - 32 - 2];
 };
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");

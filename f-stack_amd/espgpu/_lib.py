@@ -12,12 +12,14 @@ LIB_PATH = os.environ.get("ESPGPU_LIB", os.path.join(PKG_ROOT, "libespgpu.so"))
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "espgpu.h")
 
 # constants (cryptodev.h values, see include/espgpu.h)
+CSP_MODE_CIPHER = 2
 CSP_MODE_AEAD = 4
 CSP_MODE_ETA = 5
 CSP_F_SEPARATE_AAD = 0x2
 CSP_F_ESN = 0x4
 CRYPTO_SHA1_HMAC = 7
 CRYPTO_AES_CBC = 11
+CRYPTO_NULL_CBC = 16
 CRYPTO_SHA2_256_HMAC = 18
 CRYPTO_SHA2_384_HMAC = 19
 CRYPTO_SHA2_512_HMAC = 20

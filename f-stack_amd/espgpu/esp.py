@@ -17,14 +17,24 @@ CBC_SHA256, CBC_SHA384, CBC_SHA512 = ("aes-cbc-hmac-sha2-256-128", "aes-cbc-hmac
                                       "aes-cbc-hmac-sha2-512-256")
 CTR_SHA1, CTR_SHA256 = "aes-ctr-hmac-sha1-96", "aes-ctr-hmac-sha2-256-128"   # RFC 3686
 CTR_SHA384, CTR_SHA512 = "aes-ctr-hmac-sha2-384-192", "aes-ctr-hmac-sha2-512-256"
+# ESP-NULL (SADB_EALG_NULL, key.c:588; RFC 2410) with HMAC: encrypt-then-MAC
+# sessions whose cipher is CRYPTO_NULL_CBC (no key, no IV, blocksize 4)
+NULL_SHA1, NULL_SHA256 = "null-hmac-sha1-96", "null-hmac-sha2-256-128"
+NULL_SHA384, NULL_SHA512 = "null-hmac-sha2-384-192", "null-hmac-sha2-512-256"
+# encryption without authentication (esp_init's CSP_MODE_CIPHER, xform_esp.c:230-231)
+CBC, CTR = "aes-cbc", "aes-ctr"
 # auth algorithm and ICV bytes (xform_ah_authsize, xform_ah.c:117-131: 12 for
 # SHA1-96, hashsize/2 for SHA2 per RFC 4868)
 _AUTH = {CBC_SHA1: (L.CRYPTO_SHA1_HMAC, 12), CTR_SHA1: (L.CRYPTO_SHA1_HMAC, 12),
          CBC_SHA256: (L.CRYPTO_SHA2_256_HMAC, 16), CTR_SHA256: (L.CRYPTO_SHA2_256_HMAC, 16),
          CBC_SHA384: (L.CRYPTO_SHA2_384_HMAC, 24), CTR_SHA384: (L.CRYPTO_SHA2_384_HMAC, 24),
-         CBC_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32), CTR_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32)}
-_CTR_ALGS = (CTR_SHA1, CTR_SHA256, CTR_SHA384, CTR_SHA512)
+         CBC_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32), CTR_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32),
+         NULL_SHA1: (L.CRYPTO_SHA1_HMAC, 12), NULL_SHA256: (L.CRYPTO_SHA2_256_HMAC, 16),
+         NULL_SHA384: (L.CRYPTO_SHA2_384_HMAC, 24), NULL_SHA512: (L.CRYPTO_SHA2_512_HMAC, 32)}
+_CTR_ALGS = (CTR_SHA1, CTR_SHA256, CTR_SHA384, CTR_SHA512, CTR)
+_NULL_ALGS = (NULL_SHA1, NULL_SHA256, NULL_SHA384, NULL_SHA512)
 ETA_ALGS = tuple(_AUTH)
+CIPHER_ALGS = (CBC, CTR)
 IPPROTO_NONE = 59
 
 
@@ -40,23 +50,34 @@ class SecAssoc:
         # ICV bytes: xform_ah_authsize (GMAC 16, SHA1-HMAC 12, SHA2-HMAC
         # hashsize/2); a GCM SA may carry a truncated 12- or 8-byte ICV
         # (RFC 4106 s3.3, csp_auth_mlen)
-        self.mlen = mlen if mlen is not None else (16 if alg == GCM else _AUTH[alg][1])
+        self.mlen = mlen if mlen is not None else (
+            16 if alg == GCM else _AUTH[alg][1] if alg in _AUTH else 0)
 
     @property
     def ctr(self):
         return self.alg in _CTR_ALGS
 
     @property
+    def null(self):
+        return self.alg in _NULL_ALGS
+
+    @property
+    def auth(self):
+        """An ICV to verify / compute (every transform but the CIPHER ones)."""
+        return self.alg == GCM or self.alg in _AUTH
+
+    @property
     def cipher_alg(self):
-        return L.CRYPTO_AES_ICM if self.ctr else L.CRYPTO_AES_CBC
+        return L.CRYPTO_AES_ICM if self.ctr else L.CRYPTO_NULL_CBC if self.null else L.CRYPTO_AES_CBC
 
     @property
     def auth_alg(self):
-        return _AUTH[self.alg][0]
+        return _AUTH[self.alg][0] if self.alg in _AUTH else 0
 
     @property
     def ivlen(self):
-        return 8 if self.alg == GCM or self.ctr else 16       # RFC 4106 / 3686: 8-byte IV
+        # RFC 4106 / 3686: 8-byte IV; enc_xform_null: none; CBC: 16
+        return 8 if self.alg == GCM or self.ctr else 0 if self.null else 16
 
     @property
     def hlen(self):
@@ -68,7 +89,8 @@ class SecAssoc:
 
     @property
     def blocksize(self):
-        return 1 if self.alg == GCM or self.ctr else 16    # enc_xform blocksize (ESP pads to 4 anyway)
+        # enc_xform blocksize (ESP pads to 4 anyway): GCM / CTR 1, NULL 4, CBC 16
+        return 1 if self.alg == GCM or self.ctr else 4 if self.null else 16
 
     @property
     def salt(self):
@@ -83,11 +105,16 @@ class SecAssoc:
                 csp_ivlen=12, csp_cipher_alg=L.CRYPTO_AES_NIST_GCM_16,
                 csp_cipher_klen=len(self.key) - 4, csp_cipher_key=self.key[:-4],
                 csp_auth_mlen=0 if self.mlen == 16 else self.mlen)
-        ckey = self.key[:-4] if self.ctr else self.key
+        ckey = self.key[:-4] if self.ctr else b"" if self.null else self.key
+        ivsize = 0 if self.null else 16                      # csp_ivlen = txform->ivsize (:240)
+        if not self.auth:                                     # esp_init :230-231
+            return crypto_session_params(
+                csp_mode=L.CSP_MODE_CIPHER, csp_ivlen=ivsize, csp_cipher_alg=self.cipher_alg,
+                csp_cipher_klen=len(ckey), csp_cipher_key=ckey)
         return crypto_session_params(
             csp_mode=L.CSP_MODE_ETA, csp_flags=L.CSP_F_ESN if self.esn else 0,
-            csp_ivlen=16, csp_cipher_alg=self.cipher_alg, csp_cipher_klen=len(ckey),
-            csp_cipher_key=ckey, csp_auth_alg=self.auth_alg,
+            csp_ivlen=ivsize, csp_cipher_alg=self.cipher_alg, csp_cipher_klen=len(ckey),
+            csp_cipher_key=ckey if ckey else None, csp_auth_alg=self.auth_alg,
             csp_auth_klen=len(self.auth_key), csp_auth_key=self.auth_key, csp_auth_mlen=self.mlen)
 
 
@@ -99,18 +126,20 @@ def esp_input_crp(fw, ses, sa, pkt, skip, esn_hi=0):
     """Build the decrypt+verify cryptop exactly as esp_input does."""
     total = len(_flat(pkt))
     crp = fw.crypto_getreq(ses)
-    crp.crp_op = L.CRYPTO_OP_VERIFY_DIGEST | L.CRYPTO_OP_DECRYPT
-    crp.crp_aad_length = 8 if sa.alg == GCM else sa.hlen                      # :366-369
     seqh = struct.pack(">I", esn_hi)
     data = _flat(pkt)
-    if sa.alg == GCM and sa.esn:                                              # :372-397
-        crp.crp_aad = data[skip:skip + 4] + seqh + data[skip + 4:skip + 8]
-        crp.crp_aad_length = 12
-    else:
-        crp.crp_aad_start = skip
-    if sa.alg != GCM and sa.esn:
-        crp.crp_esn = seqh                                                    # :400-402
-    crp.crp_digest_start = total - sa.alen                                    # :404
+    if sa.auth:                                                               # :364-405
+        crp.crp_op = L.CRYPTO_OP_VERIFY_DIGEST
+        crp.crp_aad_length = 8 if sa.alg == GCM else sa.hlen                  # :366-369
+        if sa.alg == GCM and sa.esn:                                          # :372-397
+            crp.crp_aad = data[skip:skip + 4] + seqh + data[skip + 4:skip + 8]
+            crp.crp_aad_length = 12
+        else:
+            crp.crp_aad_start = skip
+        if sa.alg != GCM and sa.esn:
+            crp.crp_esn = seqh                                                # :400-402
+        crp.crp_digest_start = total - sa.alen                                # :404
+    crp.crp_op |= L.CRYPTO_OP_DECRYPT                                         # :420
     crp.crp_flags = L.CRYPTO_F_CBIFSYNC
     crp.crp_buf = pkt
     crp.crp_payload_start = skip + sa.hlen                                    # :424-425
@@ -119,7 +148,7 @@ def esp_input_crp(fw, ses, sa, pkt, skip, esn_hi=0):
         ctr0 = struct.pack(">I", 1) if sa.ctr else b"\0" * 4
         crp.crp_iv = bytearray(sa.salt + data[skip + sa.hlen - sa.ivlen:skip + sa.hlen] + ctr0)
         crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
-    else:
+    elif sa.ivlen:
         crp.crp_iv_start = skip + sa.hlen - sa.ivlen
     return crp
 
@@ -129,13 +158,20 @@ def esp_output_crp(fw, ses, sa, pkt, skip, esn_hi=0):
     total = len(_flat(pkt))
     data = _flat(pkt)
     crp = fw.crypto_getreq(ses)
-    crp.crp_op = L.CRYPTO_OP_ENCRYPT | L.CRYPTO_OP_COMPUTE_DIGEST
+    crp.crp_op = L.CRYPTO_OP_ENCRYPT | (L.CRYPTO_OP_COMPUTE_DIGEST if sa.auth else 0)
     crp.crp_flags = L.CRYPTO_F_CBIFSYNC
     crp.crp_buf = pkt
     crp.crp_payload_start = skip + sa.hlen
     crp.crp_payload_length = total - (skip + sa.hlen + sa.alen)
-    crp.crp_digest_start = total - sa.alen
     seqh = struct.pack(">I", esn_hi)
+    if not sa.auth:                                                   # :862-887, no esph
+        if sa.ctr:
+            crp.crp_iv = bytearray(sa.salt + data[skip + 8:skip + 16] + struct.pack(">I", 1))
+            crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
+        elif sa.ivlen:
+            crp.crp_iv_start = skip + 8
+        return crp
+    crp.crp_digest_start = total - sa.alen
     if sa.alg == GCM:
         if sa.esn:
             crp.crp_aad = data[skip:skip + 4] + seqh + data[skip + 4:skip + 8]
@@ -151,7 +187,7 @@ def esp_output_crp(fw, ses, sa, pkt, skip, esn_hi=0):
         if sa.ctr:
             crp.crp_iv = bytearray(sa.salt + data[skip + 8:skip + 16] + struct.pack(">I", 1))
             crp.crp_flags |= L.CRYPTO_F_IV_SEPARATE
-        else:
+        elif sa.ivlen:
             crp.crp_iv_start = skip + 8
         if sa.esn:
             crp.crp_esn = seqh

@@ -6,9 +6,13 @@
  * framework, i.e. it replaces the software driver "cryptosoft"
  * (freebsd/opencrypto/cryptosoft.c) for the ESP ciphers F-Stack's IPsec uses:
  *   AES-GCM-16 (CSP_MODE_AEAD)                  -> swcr_gcm      cryptosoft.c:465-645
- *   AES-CBC or AES-CTR (RFC 3686) + HMAC-SHA1-96
+ *   AES-CBC, AES-CTR (RFC 3686) or NULL + HMAC-SHA1-96
  *     or HMAC-SHA2-256-128 / -384-192 / -512-256
  *     (CSP_MODE_ETA)                            -> swcr_eta      cryptosoft.c:874-888
+ *                                                  (NULL: swcr_authcompute, :1394-1398)
+ *   AES-CBC or AES-CTR with no auth, or NULL
+ *     (CSP_MODE_CIPHER)                         -> swcr_encdec   cryptosoft.c:101-284
+ *                                                  (NULL: swcr_null, :91-95)
  * Every entry point is plain C: integers, pointers, sizes.  No exceptions,
  * no C++ or torch types cross it.  Errors are errno values, as in opencrypto.
  * One espgpu_ctx per lcore thread (thread-compatible, not thread-safe), the
@@ -41,12 +45,14 @@ extern "C" {
 #define ESPGPU_ABI_VERSION 1
 
 /* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
+#define ESPGPU_CSP_MODE_CIPHER      2        /* cryptodev.h:362: ESP without auth */
 #define ESPGPU_CSP_MODE_AEAD        4        /* cryptodev.h:364 */
 #define ESPGPU_CSP_MODE_ETA         5        /* cryptodev.h:365 */
 #define ESPGPU_CSP_F_SEPARATE_AAD   0x0002   /* cryptodev.h:370 */
 #define ESPGPU_CSP_F_ESN            0x0004   /* cryptodev.h:371 */
 #define ESPGPU_CRYPTO_SHA1_HMAC     7        /* cryptodev.h:150 */
 #define ESPGPU_CRYPTO_AES_CBC       11       /* cryptodev.h:155 */
+#define ESPGPU_CRYPTO_NULL_CBC      16       /* cryptodev.h:160: ESP-NULL (enc_xform_null) */
 #define ESPGPU_CRYPTO_SHA2_256_HMAC 18     /* cryptodev.h:162 */
 #define ESPGPU_CRYPTO_SHA2_384_HMAC 19     /* cryptodev.h:163 */
 #define ESPGPU_CRYPTO_SHA2_512_HMAC 20     /* cryptodev.h:164 */

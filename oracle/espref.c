@@ -863,7 +863,7 @@ oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int ck
 	oref_sa *sa;
 
 	init_tables();
-	if (cklen != 16 && cklen != 24 && cklen != 32)
+	if (calg == OREF_CRYPTO_NULL_CBC ? cklen != 0 : (cklen != 16 && cklen != 24 && cklen != 32))
 		return NULL;
 	sa = calloc(1, sizeof(*sa));
 	if (sa == NULL)
@@ -877,22 +877,27 @@ oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int ck
 		sa->icm.nr = oref_aes_setkey_enc(sa->icm.ek, ckey, cklen * 8);
 		if (salt)
 			memcpy(sa->salt, salt, 4);
-	} else if (mode == OREF_CSP_MODE_ETA) {         /* swcr_setup_cipher/auth */
-		if ((calg != OREF_CRYPTO_AES_CBC && calg != OREF_CRYPTO_AES_ICM) ||
-		    (aalg != OREF_CRYPTO_SHA1_HMAC && aalg != OREF_CRYPTO_SHA2_256_HMAC &&
+	} else if (mode == OREF_CSP_MODE_ETA || mode == OREF_CSP_MODE_CIPHER) {   /* swcr_setup_cipher/auth */
+		const int auth = mode == OREF_CSP_MODE_ETA;
+		if ((calg != OREF_CRYPTO_AES_CBC && calg != OREF_CRYPTO_AES_ICM && calg != OREF_CRYPTO_NULL_CBC) ||
+		    (auth && aalg != OREF_CRYPTO_SHA1_HMAC && aalg != OREF_CRYPTO_SHA2_256_HMAC &&
 		     aalg != OREF_CRYPTO_SHA2_384_HMAC && aalg != OREF_CRYPTO_SHA2_512_HMAC)) {
 			free(sa);
 			return NULL;
 		}
 		sa->calg = calg;
-		sa->aalg = aalg;
-		sa->mlen = (mlen == 0) ? hash_len(aalg) : mlen;   /* :1013-1018 */
-		sa->nr = oref_aes_setkey_enc(sa->ek, ckey, cklen * 8);
-		oref_aes_setkey_dec(sa->dk, ckey, cklen * 8);
+		sa->aalg = auth ? aalg : 0;
+		sa->mlen = !auth ? 0 : (mlen == 0) ? hash_len(aalg) : mlen;   /* :1013-1018 */
+		if (calg != OREF_CRYPTO_NULL_CBC) {
+			sa->nr = oref_aes_setkey_enc(sa->ek, ckey, cklen * 8);
+			oref_aes_setkey_dec(sa->dk, ckey, cklen * 8);
+		}
 		if (salt)
 			memcpy(sa->salt, salt, 4);      /* AES-ICM nonce (RFC 3686) */
-		h_hmac_pad(akey, aklen, &sa->ictx, aalg, 0x36);
-		h_hmac_pad(akey, aklen, &sa->octx, aalg, 0x5c);
+		if (auth) {
+			h_hmac_pad(akey, aklen, &sa->ictx, aalg, 0x36);
+			h_hmac_pad(akey, aklen, &sa->octx, aalg, 0x5c);
+		}
 	} else {
 		free(sa);
 		return NULL;
@@ -1059,6 +1064,10 @@ static int swcr_eta_c(const oref_sa *sa, struct req *r)   /* cryptosoft.c:874-88
 {
 	int e;
 
+	if (sa->mode == OREF_CSP_MODE_CIPHER)            /* swcr_encdec / swcr_null, :1339-1350 */
+		return sa->calg == OREF_CRYPTO_NULL_CBC ? 0 : swcr_encdec_cbc(sa, r);
+	if (sa->calg == OREF_CRYPTO_NULL_CBC)            /* digest only, :1394-1398 */
+		return swcr_authcompute_c(sa, r);
 	if (r->encrypt) {
 		e = swcr_encdec_cbc(sa, r);
 		return e ? e : swcr_authcompute_c(sa, r);
@@ -1075,14 +1084,18 @@ static int esp_process(const oref_sa *sa, uint8_t *esp, int len, uint32_t esn_hi
 	uint8_t aadbuf[12];
 	int gcm = (sa->mode == OREF_CSP_MODE_AEAD);
 	int ctr = !gcm && sa->calg == OREF_CRYPTO_AES_ICM;
-	int ivlen = (gcm || ctr) ? 8 : 16, hlen = 8 + ivlen;   /* RFC 4106 / 3686: 8-byte IV */
+	int null = !gcm && sa->calg == OREF_CRYPTO_NULL_CBC;
+	/* RFC 4106 / 3686: 8-byte IV; CBC 16 (txform->ivsize); NULL none */
+	int ivlen = (gcm || ctr) ? 8 : null ? 0 : 16, hlen = 8 + ivlen;
 	/* ICV bytes = the session's sw_mlen (cryptosoft.c:1112-1117): 16 for GCM
 	 * and 12 for HMAC-SHA1-96 as ESP sets them up (xform_ah_authsize), 8/12
 	 * for a truncated GCM session, 20 for an untruncated HMAC-SHA1 one */
 	int alen = sa->mlen;
 	int plen = len - hlen - alen;
 
-	if ((len & 3) || plen <= 0 || (!gcm && !ctr && (plen & 15)))   /* :279-324 */
+	/* :279-324: payload a multiple of the cipher's blocksize (CBC 16, CTR 1,
+	 * NULL 4) and records 4-byte multiples */
+	if ((len & 3) || plen <= 0 || (!gcm && !ctr && !null && (plen & 15)))
 		return EINVAL;
 	memset(&r, 0, sizeof(r));
 	r.buf = esp;

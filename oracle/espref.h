@@ -32,6 +32,7 @@ extern "C" {
 #endif
 
 /* Session modes (values of crypto_session_params.csp_mode, cryptodev.h:360-365). */
+#define OREF_CSP_MODE_CIPHER 2          /* cipher only: ESP without auth (esp_init :230-231) */
 #define OREF_CSP_MODE_AEAD 4
 #define OREF_CSP_MODE_ETA  5
 /* csp_flags (cryptodev.h:369-371) */
@@ -40,6 +41,7 @@ extern "C" {
 /* algorithms (cryptodev.h:150-169) */
 #define OREF_CRYPTO_SHA1_HMAC      7
 #define OREF_CRYPTO_AES_CBC        11
+#define OREF_CRYPTO_NULL_CBC       16     /* enc_xform_null: blocksize 4, no IV (xform_null.c:65-76) */
 #define OREF_CRYPTO_SHA2_256_HMAC  18
 #define OREF_CRYPTO_SHA2_384_HMAC  19     /* cryptodev.h:163 */
 #define OREF_CRYPTO_SHA2_512_HMAC  20     /* cryptodev.h:164 */
@@ -84,9 +86,12 @@ int oref_eta(const uint8_t *ckey, int cklen, const uint8_t *akey, int aklen,
  * ETA: AES-CBC cipher key + HMAC-SHA1 key, mlen 12 (AH_HMAC_HASHLEN). */
 oref_sa *oref_sa_new(int mode, int flags, const uint8_t *ckey, int cklen,
                      const uint8_t salt[4], const uint8_t *akey, int aklen, int mlen);
-/* ETA with a chosen cipher (OREF_CRYPTO_AES_CBC, or _AES_ICM: RFC 3686 ESP
- * AES-CTR, salt = the 4-byte nonce esp_init strips from the key) and HMAC
- * (OREF_CRYPTO_SHA1_HMAC or _SHA2_256/384/512_HMAC; mlen 0 = the full hash). */
+/* ETA with a chosen cipher (OREF_CRYPTO_AES_CBC, _AES_ICM: RFC 3686 ESP
+ * AES-CTR, salt = the 4-byte nonce esp_init strips from the key, or
+ * _NULL_CBC: no key, swcr_newsession degrades the session to the digest,
+ * cryptosoft.c:1394-1398) and HMAC (OREF_CRYPTO_SHA1_HMAC or
+ * _SHA2_256/384/512_HMAC; mlen 0 = the full hash).  CIPHER: the same ciphers
+ * with no auth (aalg 0; NULL_CBC is swcr_null, cryptosoft.c:1339-1342). */
 oref_sa *oref_sa_new2(int mode, int flags, int calg, const uint8_t *ckey, int cklen,
                       const uint8_t salt[4], int aalg, const uint8_t *akey, int aklen, int mlen);
 void oref_sa_free(oref_sa *sa);

@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libref.so")
 
+CSP_MODE_CIPHER = 2          # cryptodev.h:362, ESP without auth
 CSP_MODE_AEAD = 4
 CSP_MODE_ETA = 5
 CRYPTO_SHA1_HMAC = 7
@@ -21,6 +22,7 @@ CRYPTO_SHA2_384_HMAC = 19
 CRYPTO_SHA2_512_HMAC = 20
 HASH_LEN = {CRYPTO_SHA1_HMAC: 20, CRYPTO_SHA2_256_HMAC: 32, CRYPTO_SHA2_384_HMAC: 48, CRYPTO_SHA2_512_HMAC: 64}
 CRYPTO_AES_ICM = 23
+CRYPTO_NULL_CBC = 16         # cryptodev.h:160, enc_xform_null
 CSP_F_SEPARATE_AAD = 0x2
 CSP_F_ESN = 0x4
 EBADMSG = 74

@@ -277,6 +277,37 @@ def eta_esp_packets():
     return out
 
 
+def cipher_esp_packets():
+    """ESP packets of cipher-only SAs (esp_init's CSP_MODE_CIPHER: an
+    encryption algorithm and no authentication, xform_esp.c:230-231):
+    pkt_aes_128_cbc_null is AES-128-CBC with RTE_CRYPTO_AUTH_NULL, an ingress
+    vector, so the ESP packet is its input and the inner packet its output."""
+    path = os.path.join(TESTDIR, "test_cryptodev_security_ipsec_test_vectors.h")
+    structs = parse_structs(path, r"struct\s+ipsec_test_data")
+    out = []
+    for name in ["pkt_aes_128_cbc_null"]:
+        s = structs[name]
+        ch = s["xform"]["chain"]
+        cipher, auth = ch["cipher"]["cipher"], ch["auth"]["auth"]
+        assert cipher["algo"] == "RTE_CRYPTO_CIPHER_AES_CBC" and auth["algo"] == "RTE_CRYPTO_AUTH_NULL"
+        assert s["ipsec_xform"]["direction"] == "RTE_SECURITY_IPSEC_SA_DIR_INGRESS"
+        esp_pkt = s["input_text"]["data"][: s["input_text"]["len"]]
+        inner = s["output_text"]["data"][: s["output_text"]["len"]]
+        iphl = (esp_pkt[0] & 0xF) * 4
+        out.append({
+            "name": name,
+            "source": "dpdk/app/test/test_cryptodev_security_ipsec_test_vectors.h",
+            "mode": "cbc-null",
+            "cipher_key": hexs(data_of(s["key"], {}, cipher["key"]["length"])),
+            "iv": hexs(data_of(s["iv"], {}, cipher["iv"]["length"])),
+            "spi": s["ipsec_xform"]["spi"],
+            "outer_hdr_len": iphl,
+            "esp_record": hexs(esp_pkt[iphl:]),
+            "inner_packet": hexs(inner),
+        })
+    return out
+
+
 def ctr_hmac_sha1():
     """AES-CTR chained with HMAC-SHA1 (digest over the ciphertext); the IV is
     the whole initial counter block (16 bytes) or a 12-byte nonce whose
@@ -309,7 +340,7 @@ def main():
         return 1
     for fname, fn in (("esp_packets.json", esp_packets), ("gcm_aead.json", gcm_aead),
                       ("cbc_hmac_sha1.json", cbc_hmac_sha1), ("eta_esp_packets.json", eta_esp_packets),
-                      ("ctr_hmac_sha1.json", ctr_hmac_sha1)):
+                      ("ctr_hmac_sha1.json", ctr_hmac_sha1), ("cipher_esp_packets.json", cipher_esp_packets)):
         vecs = fn()
         with open(os.path.join(OUT, fname), "w") as f:
             json.dump(vecs, f, indent=1)

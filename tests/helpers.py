@@ -35,36 +35,46 @@ class GcmSA:
 
 
 class EtaSA:
-    """An encrypt-then-MAC SA: AES-CBC (hlen 24) or AES-CTR (RFC 3686, hlen 16,
-    salt = the nonce) with HMAC-SHA1-96 or HMAC-SHA2-256/384/512 (ICV =
-    hashsize/2, RFC 4868).  sha: 1, 256, 384 or 512 (sha256=True = 256)."""
+    """An encrypt-then-MAC SA: AES-CBC (hlen 24), AES-CTR (RFC 3686, hlen 16,
+    salt = the nonce) or ESP-NULL (null=True: CRYPTO_NULL_CBC, no key, no IV,
+    hlen 8) with HMAC-SHA1-96 or HMAC-SHA2-256/384/512 (ICV = hashsize/2,
+    RFC 4868).  sha: 1, 256, 384 or 512 (sha256=True = 256).  noauth=True:
+    the cipher alone (esp_init's CSP_MODE_CIPHER, no ICV)."""
 
     _AALG = {1: O.CRYPTO_SHA1_HMAC, 256: O.CRYPTO_SHA2_256_HMAC, 384: O.CRYPTO_SHA2_384_HMAC,
              512: O.CRYPTO_SHA2_512_HMAC}
     _MLEN = {1: 12, 256: 16, 384: 24, 512: 32}
 
-    def __init__(self, rng, klen=32, esn=False, spi=None, ctr=False, sha256=False, sha=None, aklen=None):
-        self.sha = sha if sha is not None else (256 if sha256 else 1)
-        self.key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+    def __init__(self, rng, klen=32, esn=False, spi=None, ctr=False, sha256=False, sha=None, aklen=None,
+                 null=False, noauth=False, mlen=None):
+        self.noauth, self.null = noauth, null
+        self.sha = None if noauth else sha if sha is not None else (256 if sha256 else 1)
+        self.key = b"" if null else rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
         if aklen is None:
-            aklen = {1: 20, 256: 32, 384: 48, 512: 64}[self.sha]
+            aklen = {None: 0, 1: 20, 256: 32, 384: 48, 512: 64}[self.sha]
         self.akey = rng.integers(0, 256, aklen, dtype=np.uint8).tobytes()
         self.ctr, self.sha256 = ctr, self.sha == 256
         self.salt = rng.integers(0, 256, 4, dtype=np.uint8).tobytes() if ctr else b"\0\0\0\0"
         self.spi = int(rng.integers(256, 2**32 - 1)) if spi is None else spi
-        self.esn = esn
-        self.mlen = self._MLEN[self.sha]
-        self.hlen = 16 if ctr else 24
-        self.oracle = O.SA(O.CSP_MODE_ETA, self.key, self.salt, akey=self.akey, mlen=self.mlen,
-                           calg=O.CRYPTO_AES_ICM if ctr else O.CRYPTO_AES_CBC, aalg=self._AALG[self.sha],
-                           flags=O.CSP_F_ESN if esn else 0)
+        self.esn = esn and not noauth
+        self.mlen = 0 if noauth else mlen if mlen is not None else self._MLEN[self.sha]
+        self.hlen = 16 if ctr else 8 if null else 24
+        calg = O.CRYPTO_AES_ICM if ctr else O.CRYPTO_NULL_CBC if null else O.CRYPTO_AES_CBC
+        self.oracle = O.SA(O.CSP_MODE_CIPHER if noauth else O.CSP_MODE_ETA, self.key, self.salt,
+                           akey=self.akey, mlen=self.mlen, calg=calg,
+                           aalg=0 if noauth else self._AALG[self.sha],
+                           flags=O.CSP_F_ESN if self.esn else 0)
 
     def esp_sa(self):
         from espgpu import esp as E
-        alg = {(0, 1): E.CBC_SHA1, (0, 256): E.CBC_SHA256, (0, 384): E.CBC_SHA384, (0, 512): E.CBC_SHA512,
-               (1, 1): E.CTR_SHA1, (1, 256): E.CTR_SHA256, (1, 384): E.CTR_SHA384, (1, 512): E.CTR_SHA512}
-        return E.SecAssoc(self.spi, alg[(int(self.ctr), self.sha)],
-                          self.key + (self.salt if self.ctr else b""), self.akey, esn=self.esn)
+        alg = {("cbc", 1): E.CBC_SHA1, ("cbc", 256): E.CBC_SHA256, ("cbc", 384): E.CBC_SHA384,
+               ("cbc", 512): E.CBC_SHA512, ("ctr", 1): E.CTR_SHA1, ("ctr", 256): E.CTR_SHA256,
+               ("ctr", 384): E.CTR_SHA384, ("ctr", 512): E.CTR_SHA512, ("null", 1): E.NULL_SHA1,
+               ("null", 256): E.NULL_SHA256, ("null", 384): E.NULL_SHA384, ("null", 512): E.NULL_SHA512,
+               ("cbc", None): E.CBC, ("ctr", None): E.CTR}
+        kind = "ctr" if self.ctr else "null" if self.null else "cbc"
+        return E.SecAssoc(self.spi, alg[(kind, self.sha)],
+                          self.key + (self.salt if self.ctr else b""), self.akey, esn=self.esn, mlen=self.mlen)
 
 
 def build_records(rng, sas, sa_idx, ct_lens, gcm=True, stride_pad=0, esn_hi=None, tails=None, seqs=None):

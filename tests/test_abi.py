@@ -60,6 +60,24 @@ def test_probesession_accepts_eta_variants(calg, aalg, mlen):
                       csp_auth_key=b"a" * 32, csp_auth_mlen=mlen) == L.CRYPTODEV_PROBE_HARDWARE
 
 
+@pytest.mark.parametrize("calg,klen,ivlen", [(L.CRYPTO_AES_CBC, 16, 16), (L.CRYPTO_AES_CBC, 32, 16),
+                                             (L.CRYPTO_AES_ICM, 24, 16), (L.CRYPTO_NULL_CBC, 0, 0)])
+def test_probesession_accepts_cipher_only(calg, klen, ivlen):
+    """ESP with encryption and no auth: esp_init's CSP_MODE_CIPHER
+    (xform_esp.c:230-231; swcr_probesession :1257-1266)."""
+    assert _probe(csp_mode=L.CSP_MODE_CIPHER, csp_ivlen=ivlen, csp_cipher_alg=calg, csp_cipher_klen=klen,
+                  csp_cipher_key=b"k" * klen if klen else None) == L.CRYPTODEV_PROBE_HARDWARE
+
+
+@pytest.mark.parametrize("aalg,mlen", [(L.CRYPTO_SHA1_HMAC, 12), (L.CRYPTO_SHA2_256_HMAC, 16),
+                                       (L.CRYPTO_SHA2_384_HMAC, 24), (L.CRYPTO_SHA2_512_HMAC, 32)])
+def test_probesession_accepts_esp_null(aalg, mlen):
+    """ESP-NULL with HMAC (SADB_EALG_NULL, key.c:588): CSP_MODE_ETA with
+    CRYPTO_NULL_CBC, no cipher key, csp_ivlen 0 (enc_xform_null's ivsize)."""
+    assert _probe(csp_mode=L.CSP_MODE_ETA, csp_ivlen=0, csp_cipher_alg=L.CRYPTO_NULL_CBC, csp_auth_alg=aalg,
+                  csp_auth_klen=32, csp_auth_key=b"a" * 32, csp_auth_mlen=mlen) == L.CRYPTODEV_PROBE_HARDWARE
+
+
 def test_probesession_accepts_esp_cbc_sha1():
     assert _probe(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=L.CRYPTO_AES_CBC,
                   csp_cipher_klen=32, csp_cipher_key=b"k" * 32, csp_auth_alg=L.CRYPTO_SHA1_HMAC,
@@ -84,7 +102,15 @@ def test_probesession_accepts_esp_cbc_sha1():
          csp_auth_alg=7, csp_auth_klen=20),                                                 # CTR ivlen != 16
     dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=16, csp_cipher_alg=23, csp_cipher_klen=16,
          csp_auth_alg=18, csp_auth_klen=32, csp_auth_mlen=36),                              # mlen > SHA-256
-    dict(csp_mode=2, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16),                  # cipher-only
+    dict(csp_mode=2, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16, csp_auth_alg=7,
+         csp_auth_klen=20),                                                                 # cipher-only with auth
+    dict(csp_mode=2, csp_flags=0x4, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=16),   # cipher-only with ESN
+    dict(csp_mode=2, csp_ivlen=16, csp_cipher_alg=11, csp_cipher_klen=20),                  # cipher-only, bad key
+    dict(csp_mode=2, csp_ivlen=0, csp_cipher_alg=16, csp_cipher_klen=8),                    # NULL with a key
+    dict(csp_mode=L.CSP_MODE_ETA, csp_ivlen=0, csp_cipher_alg=16, csp_cipher_klen=16,
+         csp_auth_alg=7, csp_auth_klen=20),                                                 # ESP-NULL with a key
+    dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=25, csp_cipher_klen=16,
+         csp_auth_mlen=4),                                                                  # GCM ICV 4 (not RFC 4106)
     dict(csp_mode=L.CSP_MODE_AEAD, csp_flags=0x1, csp_ivlen=12, csp_cipher_alg=25,
          csp_cipher_klen=16),                                                               # SEPARATE_OUTPUT
     dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=25, csp_cipher_klen=16,

@@ -194,14 +194,23 @@ def _variant_sas(rng, esn=False):
     return [EtaSA(rng, 16, esn=esn, ctr=c, sha256=h) for c in (False, True) for h in (False, True)] + \
            [EtaSA(rng, 32, esn=esn, ctr=True, sha256=True), EtaSA(rng, 24, esn=esn, ctr=True),
             EtaSA(rng, 16, esn=esn, sha=384), EtaSA(rng, 24, esn=esn, sha=512),
-            EtaSA(rng, 32, esn=esn, ctr=True, sha=512, aklen=150), EtaSA(rng, 16, esn=esn, ctr=True, sha=384, aklen=7)]
+            EtaSA(rng, 32, esn=esn, ctr=True, sha=512, aklen=150), EtaSA(rng, 16, esn=esn, ctr=True, sha=384, aklen=7)] + \
+           _f4_sas(rng, esn)
+
+
+def _f4_sas(rng, esn=False):
+    """The rest of key.c's ESP transforms the engine serves: encryption
+    without auth (CSP_MODE_CIPHER, AES-CBC and AES-CTR) and ESP-NULL with
+    every HMAC (CRYPTO_NULL_CBC: the payload unencrypted, only the ICV)."""
+    return [EtaSA(rng, 16, noauth=True), EtaSA(rng, 32, ctr=True, noauth=True)] + \
+           [EtaSA(rng, esn=esn, null=True, sha=h) for h in (1, 256, 384, 512)]
 
 
 def _variant_cts(rng, sas, sa_idx):
-    """CBC payloads are 16-byte multiples; CTR ones any 4-byte multiple."""
+    """CBC payloads are 16-byte multiples; CTR and NULL ones any 4-byte multiple."""
     cbc = rng.choice([16, 32, 48, 208, 1440, 1456, 8944], len(sa_idx))
     ctr = rng.choice([4, 8, 12, 20, 44, 100, 1444, 1448, 8948], len(sa_idx))
-    return np.where([sas[i].ctr for i in sa_idx], ctr, cbc)
+    return np.where([sas[i].ctr or sas[i].null for i in sa_idx], ctr, cbc)
 
 
 def _hl(sas, idx):
@@ -233,6 +242,81 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
 
 
+def _full_icv_sas(rng):
+    """Untruncated ICVs: HMAC-SHA1 with csp_auth_mlen 20 and HMAC-SHA2 with
+    csp_auth_mlen 0, which swcr_setup_auth (cryptosoft.c:1013-1018) reads as
+    the whole hash (32 / 48 / 64 bytes), plus SHA2-512 with mlen 64 given
+    explicitly; CBC, CTR and NULL ciphers."""
+    sas = [EtaSA(rng, 16, sha=1, mlen=20), EtaSA(rng, 32, ctr=True, sha=1, mlen=20, esn=True),
+           EtaSA(rng, 24, sha=256, mlen=32), EtaSA(rng, 16, ctr=True, sha=384, mlen=48),
+           EtaSA(rng, 32, sha=512, mlen=64, esn=True), EtaSA(rng, null=True, sha=512, mlen=64),
+           EtaSA(rng, null=True, sha=256, mlen=32)]
+    zero = [False, False, True, True, False, False, True]    # these go in with csp_auth_mlen 0
+    return sas, zero
+
+
+def _full_icv_sessions(drv, sas, zero):
+    sids = []
+    for s, z in zip(sas, zero):
+        csp = s.esp_sa().csp()
+        if z:
+            csp.csp_auth_mlen = 0
+        rc, sid = drv.newsession(csp)
+        assert rc == 0, drv.last_error()
+        sids.append(sid)
+    return sids
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_eta_full_hash_icv_vs_oracle(drv, inplace):
+    """Full-length HMAC ICVs (20 / 32 / 48 / 64 bytes) through the planner:
+    decrypt with bit flips (statuses and plaintext vs the oracle, rejected
+    records untouched in place) and encrypt (ciphertext and ICV vs the
+    oracle)."""
+    from espgpu.batch import decrypt_batch, encrypt_batch
+    rng = np.random.default_rng(1350 + inplace)
+    sas, zero = _full_icv_sas(rng)
+    sids = _full_icv_sessions(drv, sas, zero)
+    n = 700
+    sa_idx = rng.integers(0, len(sas), n)
+    cts = _variant_cts(rng, sas, sa_idx)
+    eh = rng.integers(0, 2**32, n, dtype=np.uint32)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, esn_hi=eh)
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    arena = _dev(plain)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, _descs_dev(d), n, st)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert (arena.cpu().numpy() == ct).all()
+
+    bad = ct.copy()
+    flip = rng.random(n) < 0.1
+    for i in np.nonzero(flip)[0]:
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        bad[o + L - 1 - int(rng.integers(0, sas[sa_idx[i]].mlen))] ^= 0x04   # inside the ICV
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+    arena = _dev(bad)
+    out = arena if inplace else torch.zeros_like(arena)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out, grouped=False)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy()
+    assert (got == ref_st).all(), np.nonzero(got != ref_st)[0][:10]
+    hl, ml = _hl(sas, sa_idx)
+    ok = got == 0
+    m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
+    res = out.cpu().numpy()
+    assert (res[m_ok] == plain[m_ok]).all()
+    if inplace:
+        m_bad = _mask_var(descs[~ok], len(bad), np.zeros((~ok).sum()), np.zeros((~ok).sum()))
+        assert (res[m_bad] == bad[m_bad]).all()
+    for s in sids:
+        drv.freesession(s)
+
+
 def test_eta_fused_knob_range(drv):
     for v in (-1, 3, 7):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == 22
@@ -255,7 +339,9 @@ def _eta_variants_decrypt(drv, esn, inplace):
         o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
         bad[o + int(rng.integers(0, L))] ^= 0x10
     ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
-    assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+    # a flipped bit fails the ICV check; without auth it decrypts (to garbage)
+    auth = np.array([not sas[i].noauth for i in sa_idx])
+    assert (ref_st[flip & auth] == O.EBADMSG).all() and (ref_st[~(flip & auth)] == 0).all()
     d = descs.copy()
     d["sa"] = [sids[s] for s in sa_idx]
     arena = _dev(bad)
@@ -269,7 +355,10 @@ def _eta_variants_decrypt(drv, esn, inplace):
     ok = got == 0
     m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
     res = out.cpu().numpy()
-    assert (res[m_ok] == plain[m_ok]).all()
+    assert (res[m_ok] == ref_out[m_ok]).all()
+    clean = ok & ~flip
+    m_clean = _mask_var(descs[clean], len(bad), hl[clean], ml[clean])
+    assert (res[m_clean] == plain[m_clean]).all()
     if inplace:
         m_bad = _mask_var(descs[~ok], len(bad), np.zeros((~ok).sum()), np.zeros((~ok).sum()))
         assert (res[m_bad] == bad[m_bad]).all()
@@ -405,6 +494,81 @@ def test_dpdk_cbc_sha2_esp_kat_opencrypto(drv, v):
     assert c.crp_etype == 0
     inner = bytes.fromhex(v["inner_packet"])
     assert bytes(pkt[skip + 24:skip + 24 + len(inner)]) == inner
+    fw.crypto_freesession(ses)
+
+
+@pytest.mark.parametrize("v", golden("cipher_esp_packets.json"), ids=lambda v: v["name"])
+def test_cipher_only_esp_kat_opencrypto(drv, v):
+    """DPDK's AES-128-CBC ESP packet with no authentication through the
+    driver path: a CSP_MODE_CIPHER session (xform_esp.c:230-231) decrypts it
+    to the inner packet and encrypts the plaintext back to the packet."""
+    from espgpu import esp as E
+    from espgpu.esp import SecAssoc, esp_input_crp, esp_output_crp
+    from espgpu.opencrypto import CryptoFramework
+    fw = CryptoFramework(drv)
+    sa = SecAssoc(v["spi"], E.CBC, bytes.fromhex(v["cipher_key"]))
+    assert sa.mlen == 0 and sa.csp().csp_mode == O.CSP_MODE_CIPHER
+    err, ses = fw.crypto_newsession(sa.csp())
+    assert err == 0
+    skip = v["outer_hdr_len"]
+    rec = bytes.fromhex(v["esp_record"])
+    pkt = bytearray(bytes(skip)) + bytearray(rec)
+    c = esp_input_crp(fw, ses, sa, pkt, skip)
+    assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+    assert c.crp_etype == 0
+    inner = bytes.fromhex(v["inner_packet"])
+    assert bytes(pkt[skip + 24:skip + 24 + len(inner)]) == inner
+    c = esp_output_crp(fw, ses, sa, pkt, skip)
+    assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+    assert c.crp_etype == 0 and bytes(pkt[skip:]) == rec
+    fw.crypto_freesession(ses)
+
+
+@pytest.mark.parametrize("alg", ["null-sha1", "null-sha256", "null-sha512"])
+def test_esp_null_opencrypto_roundtrip(drv, alg):
+    """ESP-NULL + HMAC through process/flush/poll: esp_output leaves the
+    payload as it is and appends the oracle's ICV; esp_input verifies it,
+    a flipped payload bit is EBADMSG with the packet untouched."""
+    from espgpu import esp as E
+    from espgpu.esp import SecAssoc, esp_input_crp, esp_output_crp, esp_pad
+    from espgpu.opencrypto import CryptoFramework
+    fw = CryptoFramework(drv)
+    bits = int(alg.split("sha")[1])
+    rng = np.random.default_rng(1650 + bits)
+    name = {1: E.NULL_SHA1, 256: E.NULL_SHA256, 512: E.NULL_SHA512}[bits]
+    aalg = {1: O.CRYPTO_SHA1_HMAC, 256: O.CRYPTO_SHA2_256_HMAC, 512: O.CRYPTO_SHA2_512_HMAC}[bits]
+    akey = rng.integers(0, 256, {1: 20, 256: 32, 512: 64}[bits], dtype=np.uint8).tobytes()
+    sa = SecAssoc(0x6160, name, b"", akey)
+    assert sa.hlen == 8 and sa.mlen == {1: 12, 256: 16, 512: 32}[bits]
+    err, ses = fw.crypto_newsession(sa.csp())
+    assert err == 0
+    orc = O.SA(O.CSP_MODE_ETA, b"", akey=akey, mlen=sa.mlen, calg=O.CRYPTO_NULL_CBC, aalg=aalg)
+    pkts, refs = [], []
+    for nbytes in (30, 61, 1400, 8900):
+        body = esp_pad(rng.integers(0, 256, nbytes, dtype=np.uint8).tobytes(), blocksize=4)
+        rec = sa.spi.to_bytes(4, "big") + (9).to_bytes(4, "big") + body + bytes(sa.mlen)
+        e, ref = orc.esp_encrypt(rec)
+        assert e == 0 and ref[:-sa.mlen] == rec[:-sa.mlen]
+        pkt = bytearray(bytes(20) + rec)
+        pkts.append(pkt)
+        refs.append(ref)
+        assert fw.crypto_dispatch(esp_output_crp(fw, ses, sa, pkt, 20)) == 0
+    fw.crypto_drain()
+    for pkt, ref in zip(pkts, refs):
+        assert bytes(pkt[20:]) == ref
+    crps = [esp_input_crp(fw, ses, sa, pkt, 20) for pkt in pkts]
+    bad = bytearray(pkts[1])
+    bad[40] ^= 0x02
+    before = bytes(bad)
+    crps.append(esp_input_crp(fw, ses, sa, bad, 20))
+    for c in crps:
+        assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+    for c, pkt, ref in zip(crps, pkts, refs):
+        assert c.crp_etype == 0 and bytes(pkt[20:]) == ref
+    assert crps[-1].crp_etype == O.EBADMSG and bytes(bad) == before
     fw.crypto_freesession(ses)
 
 

@@ -35,14 +35,15 @@ def _all_sas(rng):
     t = [EtaSA(rng, k, esn=e, ctr=c, sha=h) for (k, c, h) in
          ((32, False, 1), (16, True, 1), (16, False, 256), (32, True, 256), (24, False, 384), (16, True, 512))
          for e in (False, True)]
-    return g + t
+    nul = [EtaSA(rng, esn=e, null=True, sha=h) for h in (1, 256, 512) for e in (False, True)]   # ESP-NULL
+    return g + t + nul
 
 
 def _cts(rng, sas, idx):
     # GCM and CTR payloads: any 4-byte multiple; CBC: whole 16-byte blocks
     free = rng.choice([4, 12, 44, 100, 204, 1444, 1448, 2996, 8948], len(idx))
     cbc = rng.choice([16, 48, 208, 1440, 1456, 8944], len(idx))
-    is_cbc = np.array([isinstance(sas[i], EtaSA) and not sas[i].ctr for i in idx])
+    is_cbc = np.array([isinstance(sas[i], EtaSA) and not sas[i].ctr and not sas[i].null for i in idx])
     return np.where(is_cbc, cbc, free)
 
 
@@ -85,7 +86,8 @@ def test_every_session_kind_mixed_vs_oracle(drv, seed, gcm_lanes):
     odd = rng.choice(cand, 12, replace=False)
     d["len"][odd] -= 2                                   # len % 4 != 0
     want_st[odd] = O.EINVAL
-    cbc = [i for i in cand if isinstance(sas[idx[i]], EtaSA) and not sas[idx[i]].ctr and i not in odd]
+    cbc = [i for i in cand if isinstance(sas[idx[i]], EtaSA) and not sas[idx[i]].ctr and not sas[idx[i]].null
+           and i not in odd]
     short = rng.choice(cbc, min(8, len(cbc)), replace=False)
     d["len"][short] -= 4                                 # CBC payload not whole blocks
     want_st[short] = O.EINVAL

@@ -294,3 +294,61 @@ def test_esp_ctr_record_layout(aalg, mlen, klen):
         bad[-2] ^= 0x40
         e, out = sa.esp_decrypt(bytes(bad))
         assert e == O.EBADMSG and out == bytes(bad)
+
+
+@pytest.mark.parametrize("v", golden("cipher_esp_packets.json"), ids=lambda v: v["name"])
+def test_cipher_only_esp_packet_kat(v):
+    """DPDK's AES-128-CBC ESP packet with no authentication: the session
+    esp_init builds for it is CSP_MODE_CIPHER (xform_esp.c:230-231), which
+    cryptosoft serves with swcr_encdec alone (cryptosoft.c:1338-1350).
+    Decrypt gives the inner packet + self-describing padding; encrypt gives
+    the packet back."""
+    sa = O.SA(O.CSP_MODE_CIPHER, bytes.fromhex(v["cipher_key"]), calg=O.CRYPTO_AES_CBC, aalg=0)
+    rec = bytes.fromhex(v["esp_record"])
+    assert rec[8:24] == bytes.fromhex(v["iv"])
+    e, out = sa.esp_decrypt(rec)
+    assert e == 0
+    inner = bytes.fromhex(v["inner_packet"])
+    pt = out[24:]
+    assert pt[:len(inner)] == inner
+    padlen, nh = pt[-2], pt[-1]
+    assert len(pt) == len(inner) + padlen + 2 and nh == 4       # IPv4 in IPv4 tunnel
+    assert pt[len(inner):len(inner) + padlen] == bytes(range(1, padlen + 1))
+    e2, again = sa.esp_encrypt(out)
+    assert e2 == 0 and again == rec
+    # no ICV: a flipped ciphertext bit decrypts (to garbage), it is not EBADMSG
+    bad = bytearray(rec)
+    bad[-1] ^= 0x01
+    assert sa.esp_decrypt(bytes(bad))[0] == 0
+
+
+@pytest.mark.parametrize("aalg,mlen", [(O.CRYPTO_SHA1_HMAC, 12), (O.CRYPTO_SHA2_256_HMAC, 16),
+                                       (O.CRYPTO_SHA2_384_HMAC, 24), (O.CRYPTO_SHA2_512_HMAC, 32)])
+def test_null_cipher_esp_record_layout(aalg, mlen):
+    """ESP-NULL with HMAC (SADB_EALG_NULL, key.c:588): esp_init makes it
+    CSP_MODE_ETA with CRYPTO_NULL_CBC, no key and no IV (enc_xform_null:
+    blocksize 4, ivsize 0, xform_null.c:65-76), and swcr_newsession degrades
+    it to the digest (cryptosoft.c:1394-1398): hlen 8, the payload is left as
+    it is, the ICV is the HMAC over SPI || SN || payload (|| ESN high)."""
+    rng = np.random.default_rng(300 + mlen)
+    akey = rng.integers(0, 256, 40, dtype=np.uint8).tobytes()
+    for esn in (False, True):
+        sa = O.SA(O.CSP_MODE_ETA, b"", akey=akey, mlen=mlen, calg=O.CRYPTO_NULL_CBC, aalg=aalg,
+                  flags=O.CSP_F_ESN if esn else 0)
+        for plen in (4, 64, 1452):
+            hdr = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+            pt = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+            eh = int(rng.integers(0, 2**32)) if esn else 0
+            e, rec = sa.esp_encrypt(hdr + pt + bytes(mlen), esn_hi=eh)
+            assert e == 0 and rec[:8 + plen] == hdr + pt
+            msg = hdr + pt + (eh.to_bytes(4, "big") if esn else b"")
+            assert rec[8 + plen:] == O.hmac(aalg, akey, msg)[:mlen]
+            e, dec = sa.esp_decrypt(rec, esn_hi=eh)
+            assert e == 0 and dec == rec
+            bad = bytearray(rec)
+            bad[8 + plen // 2] ^= 0x20
+            e, out = sa.esp_decrypt(bytes(bad), esn_hi=eh)
+            assert e == O.EBADMSG and out == bytes(bad)
+    # payload not a multiple of the null blocksize (4): EINVAL
+    sa = O.SA(O.CSP_MODE_ETA, b"", akey=akey, mlen=mlen, calg=O.CRYPTO_NULL_CBC, aalg=aalg)
+    assert sa.esp_decrypt(bytes(8 + 6 + mlen))[0] == O.EINVAL
