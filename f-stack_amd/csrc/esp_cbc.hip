@@ -626,20 +626,18 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
       }
       if (CK == CK_CBC) {
         uint4 blk[4];
-        int i0, nb;
+        int nb;
         if (b == 0) {                       // wave-uniform: every lane is at chunk 0 together
           prev = make_uint4(m[2], m[3], m[4], m[5]);
           blk[0] = make_uint4(m[6], m[7], m[8], m[9]);
           blk[1] = make_uint4(m[10], m[11], m[12], m[13]);
           blk[2] = blk[3] = make_uint4(0, 0, 0, 0);
-          i0 = 0;
           nb = 2;
         } else {
           blk[0] = make_uint4(cy0, cy1, m[0], m[1]);
           blk[1] = make_uint4(m[2], m[3], m[4], m[5]);
           blk[2] = make_uint4(m[6], m[7], m[8], m[9]);
           blk[3] = make_uint4(m[10], m[11], m[12], m[13]);
-          i0 = 4 * (int)b - 2;
           nb = 4;
         }
         cy0 = m[14];

@@ -50,6 +50,38 @@ struct Pending {
   struct Span { uint32_t buf_off, stage_from, n; } span[2];
   int nspan;
   uint32_t seg0, nsegs;       // the request's segments, copied into Slot::segpool
+  // zero-copy: the record's start in registered host memory (device-mapped
+  // address, espgpu_register_host); 0 = gathered into the staging buffer.
+  // The record's layout there is the staged one, so span k's bytes go to
+  // zc + span[k].stage_from.
+  uint64_t zc;
+};
+
+// A request process() accepted while every staging slot was in flight
+// (set_tuning "overflow_mb"): its bytes (unless zero-copy) wait in host
+// memory and flush() moves it into the next free slot, in arrival order.
+struct OvfEntry {
+  Pending pd;                 // stage_off / seg0 index the overflow's own buffers
+  espgpu_desc d;
+  int32_t sid;
+  uint8_t op, kind;
+};
+struct Overflow {
+  std::vector<OvfEntry> ent;
+  size_t head = 0;            // first entry not yet moved into a slot
+  std::vector<uint8_t> bytes;
+  std::vector<espgpu_seg> segpool;
+  bool empty() const { return head == ent.size(); }
+  size_t footprint() const { return bytes.size() + (ent.size() - head) * sizeof(OvfEntry); }
+  void reset() { ent.clear(); head = 0; bytes.clear(); segpool.clear(); }
+};
+
+// Host memory registered with espgpu_register_host.
+struct HostRegion {
+  uintptr_t base;
+  uint64_t len;
+  uint64_t dev;               // device-mapped address of base
+  bool owned;                 // hipHostRegister'ed here (else already pinned)
 };
 
 enum { SLOT_FREE = 0, SLOT_FILLING = 1, SLOT_INFLIGHT = 2 };
@@ -63,15 +95,21 @@ struct Slot {
   int state = SLOT_FREE;
   int op = -1;                // 0 decrypt, 1 encrypt
   uint8_t *h_arena = nullptr, *d_arena = nullptr, *d_out = nullptr;
+  uint8_t *h_arena_dev = nullptr;           // h_arena's device-mapped address (xfer kernel)
   espgpu_desc *h_desc = nullptr;            // descriptors while filling
+  // the xfer kernel's span lists (pinned, read by the kernel through the
+  // mapping): [0, nin) before the crypto kernels, [nin, nin + nout) after
+  XferSpan *h_xfer = nullptr, *h_xfer_dev = nullptr;
+  uint32_t xfer_cap = 0;
   uint32_t nrec = 0, bytes = 0;
+  uint32_t nstaged = 0;                     // records gathered (not zero-copy)
   uint32_t desc_off = 0, stat_off = 0;      // set by flush
   int32_t sid0 = -1;                        // session of the first record
   bool mixed = false;                       // more than one session staged
   uint32_t kinds = 0;                       // 1: GCM records, 2: ETA records
   std::vector<Pending> reqs;             // reserved to batch_records: no per-record allocation
   std::vector<espgpu_seg> segpool;       // segment lists of the staged requests
-  hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
+  hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, kout = nullptr, done = nullptr;
   hipStream_t st = nullptr;                 // small batches: copy, kernel, copy in order here
 };
 
@@ -118,6 +156,10 @@ struct espgpu_ctx {
   // staging
   std::vector<Slot> slots;
   int cur = 0;
+  Overflow ovf;
+  size_t ovf_cap = 0;            // set_tuning "overflow_mb" (0: ERESTART when the slots are busy)
+  int xfer_small = 1;            // small batches: staging region moved by the xfer kernel (else hipMemcpyAsync)
+  std::vector<HostRegion> regions;   // sorted by base
   // completions not yet handed to poll(): ready[ready_head..] (host-side
   // rejects and finished batches), reserved so steady state does not allocate
   std::vector<espgpu_completion> ready;
@@ -212,6 +254,7 @@ int alloc_slot(espgpu_ctx *c, Slot &s) {
   const size_t recs = c->cfg.batch_records;
   const size_t bytes = c->cfg.batch_bytes + 64 + recs * (sizeof(espgpu_desc) + 1) + 64;
   HIPCHK(c, hipHostMalloc((void **)&s.h_arena, bytes, hipHostMallocDefault));
+  HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_arena_dev, s.h_arena, 0));
   s.h_desc = new espgpu_desc[recs];
   HIPCHK(c, hipMalloc(&s.d_arena, bytes));
   HIPCHK(c, hipMalloc(&s.d_out, bytes));
@@ -219,6 +262,7 @@ int alloc_slot(espgpu_ctx *c, Slot &s) {
   HIPCHK(c, hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming));
   HIPCHK(c, hipEventCreate(&s.k0));
   HIPCHK(c, hipEventCreate(&s.k1));
+  HIPCHK(c, hipEventCreateWithFlags(&s.kout, hipEventDisableTiming));
   HIPCHK(c, hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
   s.reqs.reserve(recs);
   s.segpool.reserve(recs * 2);
@@ -226,15 +270,69 @@ int alloc_slot(espgpu_ctx *c, Slot &s) {
 }
 
 void free_slot(Slot &s) {
+  if (s.st) hipStreamSynchronize(s.st);
   hipHostFree(s.h_arena);
+  hipHostFree(s.h_xfer);
   delete[] s.h_desc;
   hipFree(s.d_arena); hipFree(s.d_out);
-  for (hipEvent_t e : {s.done, s.in_done, s.k0, s.k1})
+  for (hipEvent_t e : {s.done, s.in_done, s.k0, s.k1, s.kout})
     if (e) hipEventDestroy(e);
-  if (s.st) {
-    hipStreamSynchronize(s.st);
-    hipStreamDestroy(s.st);
+  if (s.st) hipStreamDestroy(s.st);
+}
+
+// The device-mapped address of [p, p + n) if it lies in one registered region, else 0.
+uint64_t region_dev(const espgpu_ctx *c, const uint8_t *p, uint32_t n) {
+  const uintptr_t a = (uintptr_t)p;
+  auto it = std::upper_bound(c->regions.begin(), c->regions.end(), a,
+                             [](uintptr_t v, const HostRegion &r) { return v < r.base; });
+  if (it == c->regions.begin()) return 0;
+  --it;
+  if (a + n > it->base + it->len) return 0;
+  return it->dev + (a - it->base);
+}
+
+// [off, off + n) of a segmented buffer if it lies in one segment, else nullptr.
+const uint8_t *seg_span(const espgpu_seg *segs, uint32_t nsegs, uint32_t off, uint32_t n) {
+  for (uint32_t i = 0; i < nsegs; ++i) {
+    if (off >= segs[i].len) { off -= segs[i].len; continue; }
+    return off + n <= segs[i].len ? (const uint8_t *)segs[i].base + off : nullptr;
   }
+  return nullptr;
+}
+
+// Append one request to a slot (its record bytes, unless zero-copy, already
+// at h_arena + bytes).
+void slot_commit(Slot &s, Pending pd, espgpu_desc d, const espgpu_seg *segs, int32_t sid, int op,
+                 uint32_t kind) {
+  if (s.state == SLOT_FREE) {
+    s.state = SLOT_FILLING;
+    s.op = op;
+    s.nrec = 0;
+    s.bytes = 0;
+    s.nstaged = 0;
+    s.reqs.clear();
+    s.segpool.clear();
+    s.sid0 = sid;
+    s.mixed = false;
+    s.kinds = 0;
+  }
+  pd.rec = s.nrec;
+  pd.stage_off = s.bytes;
+  pd.seg0 = (uint32_t)s.segpool.size();
+  s.segpool.insert(s.segpool.end(), segs, segs + pd.nsegs);
+  d.off4 = s.bytes / 4;
+  s.h_desc[s.nrec] = d;
+  s.bytes += (pd.stage_len + 15) & ~15u;
+  s.nrec++;
+  s.nstaged += pd.zc ? 0 : 1;
+  s.mixed |= (sid != s.sid0);
+  s.kinds |= kind;
+  s.reqs.push_back(pd);
+}
+
+bool slot_full(const espgpu_ctx *c, const Slot &s, int op, uint32_t rlen) {
+  return s.state == SLOT_FILLING &&
+         (s.op != op || s.nrec >= c->cfg.batch_records || s.bytes + rlen + 16 > c->cfg.batch_bytes);
 }
 
 // Launch the crypto kernels for one batch of device-resident records.
@@ -385,6 +483,8 @@ void espgpu_fini(espgpu_ctx *c) {
   for (hipStream_t st : {c->s_in, c->stream, c->s_out})
     if (st) hipStreamSynchronize(st);
   for (auto &s : c->slots) free_slot(s);
+  for (const HostRegion &r : c->regions)
+    if (r.owned) hipHostUnregister((void *)r.base);
   hipFree(c->e2e_arena); hipFree(c->e2e_out); hipFree(c->e2e_status); hipFree(c->e2e_desc);
   for (int k = 0; k < 2; ++k) {
     if (c->e2e_in[k]) hipEventDestroy(c->e2e_in[k]);
@@ -553,9 +653,11 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
 
 void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   if (!c || sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return;
-  // Requests already staged were accepted under this key: launch them now,
-  // then wait, so neither they nor flushed batches see the slot reused.
-  espgpu_flush(c);
+  // Requests already staged were accepted under this key: launch them now
+  // (and the overflow behind them), then wait, so neither they nor flushed
+  // batches see the slot reused.
+  if (c->ovf.empty()) espgpu_flush(c);
+  else espgpu_drain(c);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
   for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
@@ -578,15 +680,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
 int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   (void)hint;
   if (!c || !r) return ESPGPU_EINVAL;
-  Slot *s = &c->slots[c->cur];
-  if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ESPGPU_ERESTART; }
   const int op = (r->crp_op & ESPGPU_CRYPTO_OP_ENCRYPT) ? 1 : 0;
-  if (s->state == SLOT_FILLING && s->op != op) {
-    int e = espgpu_flush(c);
-    if (e) return e;
-    s = &c->slots[c->cur];
-    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ESPGPU_ERESTART; }
-  }
   auto reject = [&](int etype) {
     c->ready.push_back(espgpu_completion{r->opaque, etype});
     if (etype == ESPGPU_EINVAL) c->stats.einval++;
@@ -658,43 +752,36 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   }
   if (alen && r->crp_digest_start != r->crp_payload_start + plen) return reject(ESPGPU_EINVAL);
   const uint32_t rlen = (uint32_t)(hlen + plen + alen);
-  if (rlen > 65535 || (rlen & 3)) return reject(ESPGPU_EINVAL);
-  if (s->nrec >= c->cfg.batch_records || s->bytes + rlen + 16 > c->cfg.batch_bytes) {
-    int e = espgpu_flush(c);
-    if (e) return e;
-    s = &c->slots[c->cur];
-    if (s->state == SLOT_INFLIGHT) { c->stats.erestart++; return ESPGPU_ERESTART; }
+  if (rlen > 65535 || (rlen & 3) || rlen + 16 > c->cfg.batch_bytes) return reject(ESPGPU_EINVAL);
+  // Zero-copy when the whole record lies in one segment of registered memory
+  // with the layout the kernels read (the staged path takes a GCM record's
+  // header and IV from crp_aad / crp_iv: they must equal the buffer's).
+  const uint32_t rec_start = (uint32_t)(r->crp_payload_start - hlen);
+  uint64_t zc = 0;
+  if (!c->regions.empty()) {
+    const uint8_t *rp = seg_span(r->segs, (uint32_t)r->nsegs, rec_start, rlen);
+    if (rp && (!gcm || (memcmp(rp, hdr, 8) == 0 && memcmp(rp + 8, r->crp_iv + 4, 8) == 0)))
+      zc = region_dev(c, rp, rlen);
   }
-  if (s->state == SLOT_FREE) {
-    s->state = SLOT_FILLING;
-    s->op = op;
-    s->nrec = 0;
-    s->bytes = 0;
-    s->reqs.clear();
-    s->segpool.clear();
-    s->sid0 = sid;
-    s->mixed = false;
-    s->kinds = 0;
-  }
+  // the record bytes as the kernels read them: SPI | SN | IV | payload | ICV
+  auto gather = [&](uint8_t *dst) {
+    if (gcm) {
+      memcpy(dst, hdr, 8);
+      memcpy(dst + 8, r->crp_iv + 4, 8);
+      return seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)r->crp_payload_start, (uint32_t)(plen + alen),
+                          dst + hlen);
+    }
+    return seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)aad_start, rlen, dst);
+  };
   Pending pd;
   pd.opaque = r->opaque;
   pd.etype_pre = -1;
-  pd.rec = s->nrec;
-  pd.stage_off = s->bytes;
+  pd.rec = 0;
+  pd.stage_off = 0;
   pd.stage_len = rlen;
-  uint8_t *dst = s->h_arena + s->bytes;
-  bool ok;
-  if (gcm) {
-    memcpy(dst, hdr, 8);
-    memcpy(dst + 8, r->crp_iv + 4, 8);
-    ok = seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)r->crp_payload_start, (uint32_t)(plen + alen), dst + hlen);
-  } else {
-    ok = seg_copy_out(r->segs, (uint32_t)r->nsegs, (uint32_t)aad_start, rlen, dst);
-  }
-  if (!ok) return reject(ESPGPU_EINVAL);
-  pd.seg0 = (uint32_t)s->segpool.size();
   pd.nsegs = (uint32_t)r->nsegs;
-  s->segpool.insert(s->segpool.end(), r->segs, r->segs + r->nsegs);
+  pd.seg0 = 0;
+  pd.zc = zc;
   // results: payload (+ digest when encrypting) go back to the request buffer
   pd.nspan = 1;
   pd.span[0] = {(uint32_t)r->crp_payload_start, (uint32_t)hlen, (uint32_t)plen};
@@ -702,23 +789,55 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
     pd.nspan = 2;
     pd.span[1] = {(uint32_t)r->crp_digest_start, (uint32_t)(hlen + plen), (uint32_t)ses.mlen};
   }
-  espgpu_desc &d = s->h_desc[s->nrec];
-  d.off4 = s->bytes / 4;
+  espgpu_desc d;
+  d.off4 = 0;
   d.len = (uint16_t)rlen;
   d.sa = (uint16_t)sid;
   d.esn_hi = esn_hi;
   d.salt = salt;
-  s->bytes += (rlen + 15) & ~15u;
-  s->nrec++;
-  s->mixed |= (sid != s->sid0);
-  s->kinds |= gcm ? 1u : 2u;
-  s->reqs.push_back(pd);
+  const uint8_t kind = gcm ? 1 : 2;
+  // Where it goes: the filling slot; the overflow when the slots are all in
+  // flight (or the overflow already holds requests: arrival order is kept);
+  // else ERESTART.
+  Slot *s = &c->slots[c->cur];
+  bool to_ovf = !c->ovf.empty();
+  if (!to_ovf) {
+    if (slot_full(c, *s, op, rlen)) {
+      int e = espgpu_flush(c);
+      if (e) return e;
+      s = &c->slots[c->cur];
+    }
+    if (s->state == SLOT_INFLIGHT) {
+      if (!c->ovf_cap) { c->stats.erestart++; return ESPGPU_ERESTART; }
+      to_ovf = true;
+    }
+  }
+  if (to_ovf) {
+    Overflow &o = c->ovf;
+    const size_t add = (zc ? 0 : ((rlen + 15) & ~15u)) + sizeof(OvfEntry);
+    if (o.footprint() + add > c->ovf_cap) { c->stats.erestart++; return ESPGPU_ERESTART; }
+    pd.stage_off = (uint32_t)o.bytes.size();
+    if (!zc) {
+      o.bytes.resize(o.bytes.size() + ((rlen + 15) & ~15u));
+      if (!gather(o.bytes.data() + pd.stage_off)) {
+        o.bytes.resize(pd.stage_off);
+        return reject(ESPGPU_EINVAL);
+      }
+    }
+    pd.seg0 = (uint32_t)o.segpool.size();
+    o.segpool.insert(o.segpool.end(), r->segs, r->segs + r->nsegs);
+    o.ent.push_back(OvfEntry{pd, d, sid, (uint8_t)op, kind});
+    c->stats.overflow++;
+    return 0;
+  }
+  if (!zc && !gather(s->h_arena + s->bytes)) return reject(ESPGPU_EINVAL);
+  slot_commit(*s, pd, d, r->segs, sid, op, kind);
   return 0;
 }
 
-int espgpu_flush(espgpu_ctx *c) {
-  if (!c) return ESPGPU_EINVAL;
-  Slot &s = c->slots[c->cur];
+// Launch one filled slot: its staging region and zero-copy records in, the
+// crypto kernels, the results out; then the next slot becomes current.
+static int launch_slot(espgpu_ctx *c, Slot &s) {
   if (s.state != SLOT_FILLING || s.nrec == 0) return 0;
   // [records][16 B slack][descriptors][status]: one H2D on s_in -> kernels on
   // the compute stream -> one D2H on s_out, chained by events, so consecutive
@@ -727,22 +846,75 @@ int espgpu_flush(espgpu_ctx *c) {
   s.stat_off = s.desc_off + s.nrec * (uint32_t)sizeof(espgpu_desc);
   memset(s.h_arena + s.bytes, 0, 16);
   memcpy(s.h_arena + s.desc_off, s.h_desc, s.nrec * sizeof(espgpu_desc));
-  // A small batch (an RX burst) runs copy, kernel, copy in order on its
-  // slot's own stream: cross-stream event hand-offs cost more latency than
-  // the copies; the next slot's burst overlaps on the other slot's stream
-  // (kernels stay ordered through run_batch's last-launch event).  Large
+  // A small batch (an RX burst) runs in order on its slot's own stream:
+  // cross-stream event hand-offs cost more latency than the copies; the next
+  // slot's burst overlaps on the other slot's stream (kernels stay ordered
+  // through run_batch's last-launch event).  Its staging region moves by the
+  // xfer kernel (set_tuning "xfer", default) or hipMemcpyAsync.  Large
   // batches use the three ctx streams so batch k+1's H2D overlaps batch k's
-  // kernels and batch k-1's D2H.
+  // kernels and batch k-1's D2H.  Zero-copy records move by the xfer kernel
+  // on the compute stream either way.
   const bool small = s.stat_off <= kSmallBatchBytes;
+  const bool kcopy = small && c->xfer_small;
   hipStream_t s_k = small ? s.st : c->stream;
   hipStream_t s_in = small ? s.st : c->s_in, s_out = small ? s.st : c->s_out;
-  HIPCHK(c, hipMemcpyAsync(s.d_arena, s.h_arena, s.stat_off, hipMemcpyHostToDevice, s_in));
-  if (!small) {
-    HIPCHK(c, hipEventRecord(s.in_done, s_in));
-    HIPCHK(c, hipStreamWaitEvent(s_k, s.in_done, 0));
-  }
-  hipEventRecord(s.k0, s_k);
   uint8_t *dres = s.op ? s.d_arena : s.d_out;      // records out: in place (encrypt) or d_out
+  // region the copies move: all of it, or without records if every one is zero-copy
+  const uint32_t in_lo = s.nstaged ? 0 : s.desc_off, out_lo = s.nstaged ? 0 : s.stat_off;
+  const uint32_t out_hi = s.stat_off + s.nrec;
+  auto pieces = [](uint32_t n) { return (n + kXferPiece - 1) / kXferPiece; };
+  uint32_t nin = 0, nout = 0;
+  for (const Pending &pd : s.reqs) {
+    if (pd.zc) {
+      nin += pieces(pd.stage_len);
+      for (int k = 0; k < pd.nspan; ++k) nout += pieces(pd.span[k].n);
+    } else if (kcopy) {
+      nin += pieces(pd.stage_len);
+      nout += pieces(pd.stage_len);
+    }
+  }
+  if (kcopy) {
+    nin += pieces(s.stat_off - s.desc_off);
+    nout += pieces(s.nrec);
+  }
+  if (nin + nout > s.xfer_cap) {
+    hipHostFree(s.h_xfer);
+    s.h_xfer = nullptr;
+    s.xfer_cap = 0;
+    const uint32_t cap = std::max(nin + nout, 256u) * 2;
+    HIPCHK(c, hipHostMalloc((void **)&s.h_xfer, (size_t)cap * sizeof(XferSpan), hipHostMallocDefault));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_xfer_dev, s.h_xfer, 0));
+    s.xfer_cap = cap;
+  }
+  uint32_t k = 0;
+  auto add = [&](uint64_t src, uint64_t dst, uint32_t n, uint32_t rec) {
+    for (uint32_t o = 0; o < n; o += kXferPiece)
+      s.h_xfer[k++] = XferSpan{src + o, dst + o, std::min(kXferPiece, n - o), rec};
+  };
+  const uint64_t ha = (uint64_t)(uintptr_t)s.h_arena_dev, da = (uint64_t)(uintptr_t)s.d_arena;
+  const uint64_t dr = (uint64_t)(uintptr_t)dres;
+  for (const Pending &pd : s.reqs)
+    if (pd.zc) add(pd.zc, da + pd.stage_off, pd.stage_len, ~0u);
+    else if (kcopy) add(ha + pd.stage_off, da + pd.stage_off, pd.stage_len, ~0u);
+  if (kcopy) add(ha + s.desc_off, da + s.desc_off, s.stat_off - s.desc_off, ~0u);
+  // results: only for records whose status is 0 (complete_slot's rule)
+  for (const Pending &pd : s.reqs)
+    if (pd.zc)
+      for (int q = 0; q < pd.nspan; ++q)
+        add(dr + pd.stage_off + pd.span[q].stage_from, pd.zc + pd.span[q].stage_from, pd.span[q].n, pd.rec);
+    else if (kcopy) add(dr + pd.stage_off, ha + pd.stage_off, pd.stage_len, pd.rec);
+  if (kcopy) add(dr + s.stat_off, ha + s.stat_off, s.nrec, ~0u);
+  const uint8_t *d_stat = dres + s.stat_off;
+
+  if (!kcopy) {
+    HIPCHK(c, hipMemcpyAsync(s.d_arena + in_lo, s.h_arena + in_lo, s.stat_off - in_lo, hipMemcpyHostToDevice, s_in));
+    if (!small) {
+      HIPCHK(c, hipEventRecord(s.in_done, s_in));
+      HIPCHK(c, hipStreamWaitEvent(s_k, s.in_done, 0));
+    }
+  }
+  if (nin && launch_xfer(s.h_xfer_dev, nin, nullptr, s_k)) return fail(c, ESPGPU_EIO, "xfer kernel launch failed");
+  hipEventRecord(s.k0, s_k);
   // a single-session batch skips the device planner (ESPGPU_BATCH_GROUPED:
   // one session trivially satisfies "one session per chunk")
   int e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
@@ -750,12 +922,43 @@ int espgpu_flush(espgpu_ctx *c) {
                     s.op, s_k, nullptr, s.kinds);
   if (e) return e;
   hipEventRecord(s.k1, s_k);
-  if (!small) HIPCHK(c, hipStreamWaitEvent(s_out, s.k1, 0));
-  HIPCHK(c, hipMemcpyAsync(s.h_arena, dres, s.stat_off + s.nrec, hipMemcpyDeviceToHost, s_out));
-  HIPCHK(c, hipEventRecord(s.done, s_out));
+  if (nout && launch_xfer(s.h_xfer_dev + nin, nout, d_stat, s_k)) return fail(c, ESPGPU_EIO, "xfer kernel launch failed");
+  if (!kcopy) {
+    if (!small) {
+      HIPCHK(c, hipEventRecord(s.kout, s_k));
+      HIPCHK(c, hipStreamWaitEvent(s_out, s.kout, 0));
+    }
+    HIPCHK(c, hipMemcpyAsync(s.h_arena + out_lo, dres + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, s_out));
+  }
+  HIPCHK(c, hipEventRecord(s.done, kcopy ? s_k : s_out));
   s.state = SLOT_INFLIGHT;
   c->stats.batches++;
+  c->stats.zerocopy += s.nrec - s.nstaged;
   c->cur = (c->cur + 1) % (int)c->slots.size();
+  return 0;
+}
+
+int espgpu_flush(espgpu_ctx *c) {
+  if (!c) return ESPGPU_EINVAL;
+  // the filling slot, then the overflow (oldest first) into the free slots
+  Overflow &o = c->ovf;
+  for (;;) {
+    Slot &s = c->slots[c->cur];
+    if (s.state == SLOT_FILLING) {
+      int e = launch_slot(c, s);
+      if (e) return e;
+      continue;
+    }
+    if (o.empty() || s.state != SLOT_FREE) break;
+    while (!o.empty()) {
+      const OvfEntry &en = o.ent[o.head];
+      if (slot_full(c, s, en.op, en.pd.stage_len)) break;
+      if (!en.pd.zc) memcpy(s.h_arena + s.bytes, o.bytes.data() + en.pd.stage_off, en.pd.stage_len);
+      slot_commit(s, en.pd, en.d, o.segpool.data() + en.pd.seg0, en.sid, en.op, en.kind);
+      o.head++;
+    }
+  }
+  if (o.empty() && !o.ent.empty()) o.reset();
   return 0;
 }
 
@@ -769,7 +972,7 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
     int et = pd.etype_pre >= 0 ? pd.etype_pre : (int)s.h_arena[s.stat_off + pd.rec];
     if (et == 0) {
       const uint8_t *src = s.h_arena + pd.stage_off;
-      for (int k = 0; k < pd.nspan; ++k)
+      for (int k = 0; k < pd.nspan && !pd.zc; ++k)     // zero-copy: the xfer kernel wrote them
         seg_copy_in(s.segpool.data() + pd.seg0, pd.nsegs, pd.span[k].buf_off, pd.span[k].n,
                     src + pd.span[k].stage_from);
       c->stats.bytes += pd.span[0].n;
@@ -811,15 +1014,55 @@ int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
 
 int espgpu_drain(espgpu_ctx *c) {
   if (!c) return ESPGPU_EINVAL;
-  int e = espgpu_flush(c);
-  if (e) return e;
-  // oldest first (slot cur is the next to fill, so cur+1.. are older batches)
-  for (size_t k = 0; k < c->slots.size(); ++k) {
-    Slot &s = c->slots[(c->cur + k) % c->slots.size()];
-    if (s.state != SLOT_INFLIGHT) continue;
-    HIPCHK(c, hipEventSynchronize(s.done));
-    complete_slot(c, s);
+  do {
+    int e = espgpu_flush(c);
+    if (e) return e;
+    // oldest first (slot cur is the next to fill, so cur+1.. are older batches)
+    for (size_t k = 0; k < c->slots.size(); ++k) {
+      Slot &s = c->slots[(c->cur + k) % c->slots.size()];
+      if (s.state != SLOT_INFLIGHT) continue;
+      HIPCHK(c, hipEventSynchronize(s.done));
+      complete_slot(c, s);
+    }
+  } while (!c->ovf.empty());     // the overflow goes into the slots just freed
+  return 0;
+}
+
+int espgpu_register_host(espgpu_ctx *c, void *base, uint64_t len) {
+  if (!c || !base || !len) return ESPGPU_EINVAL;
+  const uintptr_t b = (uintptr_t)base;
+  for (const HostRegion &r : c->regions)
+    if (b < r.base + r.len && r.base < b + len) return fail(c, ESPGPU_EINVAL, "overlaps a registered region");
+  bool owned = true;
+  hipError_t e = hipHostRegister(base, len, hipHostRegisterMapped);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    owned = false;                   // already pinned (hipHostMalloc): only map it
+    (void)hipGetLastError();
+  } else if (e != hipSuccess) {
+    return fail(c, ESPGPU_EIO, "hipHostRegister: %s", hipGetErrorString(e));
   }
+  void *dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, base, 0) != hipSuccess || !dp) {
+    if (owned) hipHostUnregister(base);
+    return fail(c, ESPGPU_EIO, "hipHostGetDevicePointer failed");
+  }
+  HostRegion r{b, len, (uint64_t)(uintptr_t)dp, owned};
+  c->regions.insert(std::upper_bound(c->regions.begin(), c->regions.end(), r,
+                                     [](const HostRegion &x, const HostRegion &y) { return x.base < y.base; }),
+                    r);
+  return 0;
+}
+
+int espgpu_unregister_host(espgpu_ctx *c, void *base) {
+  if (!c) return ESPGPU_EINVAL;
+  auto it = std::find_if(c->regions.begin(), c->regions.end(),
+                         [&](const HostRegion &r) { return r.base == (uintptr_t)base; });
+  if (it == c->regions.end()) return ESPGPU_EINVAL;
+  // requests staged from it run to completion first (their completions wait for poll)
+  int e = espgpu_drain(c);
+  if (e) return e;
+  if (it->owned) hipHostUnregister(base);
+  c->regions.erase(it);
   return 0;
 }
 
@@ -987,6 +1230,16 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!strcmp(key, "gcm_lanes")) {
     if (value != 0 && value != kGcmLanesPerRec && value != kGcmLanesSmall) return ESPGPU_EINVAL;
     c->gcm_lanes = value;
+    return 0;
+  }
+  if (!strcmp(key, "overflow_mb")) {
+    if (value < 0 || value > 65536) return ESPGPU_EINVAL;
+    c->ovf_cap = (size_t)value << 20;
+    return 0;
+  }
+  if (!strcmp(key, "xfer")) {
+    if (value != 0 && value != 1) return ESPGPU_EINVAL;
+    c->xfer_small = value;
     return 0;
   }
   if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;

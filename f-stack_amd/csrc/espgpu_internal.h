@@ -1,5 +1,6 @@
 // espgpu_internal.h — device-side data layouts shared by the host runtime
-// (espgpu.cpp) and the HIP kernels (esp_gcm.hip, esp_cbc.hip, plan.hip).
+// (espgpu.cpp) and the HIP kernels (esp_gcm.hip, esp_cbc.hip, plan.hip,
+// xfer.hip).
 #pragma once
 #include <stdint.h>
 
@@ -118,6 +119,16 @@ __host__ __device__ inline uint32_t esp_trailer_word(uint32_t wlast, uint32_t pl
   return t;
 }
 
+// One copy of the opencrypto path's staging transfers (xfer.hip): len bytes
+// from src to dst (device or host-mapped addresses); rec != ~0u: only if
+// status[rec] == 0.  The host splits spans into pieces of at most kXferPiece
+// bytes, one workgroup each.
+struct XferSpan {
+  uint64_t src, dst;
+  uint32_t len, rec;
+};
+constexpr uint32_t kXferPiece = 4096;
+
 // Launchers (defined in the .hip files, called by espgpu.cpp).
 // lanes: 0 = by batch size (kGcmLanesSmall below kGcmSmallBatch records,
 // else kGcmLanesPerRec), or force 4 / 8 (set_tuning "gcm_lanes", tests)
@@ -130,6 +141,7 @@ int set_eta_opts(uint32_t opts);
 int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream);
 int launch_replay_check(const uint8_t *arena, espgpu_desc *desc, uint32_t n, const espgpu_replay *rp,
                         uint32_t nrp, const uint32_t *bitmap, uint8_t *rstatus, void *stream);
+int launch_xfer(const XferSpan *spans, uint32_t nspans, const uint8_t *status, void *stream);
 int launch_replay_merge(uint8_t *status, const uint8_t *rstatus, uint32_t n, void *stream);
 int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,

@@ -92,7 +92,7 @@ class Config(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("bytes", C.c_uint64), ("auth_fail", C.c_uint64),
                 ("einval", C.c_uint64), ("batches", C.c_uint64), ("kernel_ns", C.c_uint64),
-                ("erestart", C.c_uint64)]
+                ("erestart", C.c_uint64), ("overflow", C.c_uint64), ("zerocopy", C.c_uint64)]
 
 
 _lib = None
@@ -131,6 +131,8 @@ def lib():
         L.espgpu_poll.argtypes = [vp, C.POINTER(Completion), C.c_int]
         L.espgpu_drain.argtypes = [vp]
         L.espgpu_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.espgpu_register_host.argtypes = [vp, vp, C.c_uint64]
+        L.espgpu_unregister_host.argtypes = [vp, vp]
         L.espgpu_decrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint32, vp]
         L.espgpu_encrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp]
         L.espgpu_decrypt_batch_trailer.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint32, vp]

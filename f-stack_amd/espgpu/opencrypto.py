@@ -183,10 +183,33 @@ class GpuCryptoDriver:
         if rc:
             raise RuntimeError("espgpu_drain: %s" % self.last_error())
 
+    def set_tuning(self, key, value):
+        return self.lib.espgpu_set_tuning(self.ctx, key.encode(), value)
+
+    def register_host(self, arr):
+        """Register a host buffer (numpy array / bytearray) that request
+        buffers live in: its records are moved by the GPU, not gathered
+        (espgpu_register_host).  Keep `arr` alive until unregister_host."""
+        addr, n = _addr_len(arr)
+        rc = self.lib.espgpu_register_host(self.ctx, addr, n)
+        if rc:
+            raise RuntimeError("espgpu_register_host: %s" % self.last_error())
+
+    def unregister_host(self, arr):
+        rc = self.lib.espgpu_unregister_host(self.ctx, _addr_len(arr)[0])
+        if rc:
+            raise RuntimeError("espgpu_unregister_host: %d" % rc)
+
     def stats(self):
         s = L.Stats()
         self.lib.espgpu_get_stats(self.ctx, C.byref(s))
         return {k: getattr(s, k) for k, _ in L.Stats._fields_}
+
+
+def _addr_len(arr):
+    if hasattr(arr, "ctypes"):                     # numpy
+        return arr.ctypes.data, arr.nbytes
+    return C.addressof((C.c_char * len(arr)).from_buffer(arr)), len(arr)
 
 
 # ---------------------------------------------------------------------------

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define ESPGPU_ABI_VERSION 1
+#define ESPGPU_ABI_VERSION 2
 
 /* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
 #define ESPGPU_CSP_MODE_CIPHER      2        /* cryptodev.h:362: ESP without auth */
@@ -85,6 +85,7 @@ extern "C" {
 #define ESPGPU_EBADMSG  74    /* ICV mismatch (status byte / crp_etype)        */
 #define ESPGPU_ERESTART 85    /* process(): staging full, requeue (cc_qblocked) */
 #define ESPGPU_ENOTSUP  95
+#define ESPGPU_ENOBUFS  105   /* F-Stack mode: host overflow full, request dropped */
 
 /* Mirror of struct crypto_session_params (cryptodev.h:357-384). */
 struct espgpu_session_params {
@@ -157,6 +158,8 @@ struct espgpu_stats {
 	uint64_t records, bytes, auth_fail, einval;
 	uint64_t batches, kernel_ns;   /* kernel_ns: device time measured with events */
 	uint64_t erestart;
+	uint64_t overflow;             /* requests staged through the host overflow      */
+	uint64_t zerocopy;             /* records moved from / to registered memory      */
 };
 
 typedef struct espgpu_ctx espgpu_ctx;
@@ -183,22 +186,44 @@ int  espgpu_newsession(espgpu_ctx *ctx, const struct espgpu_session_params *csp,
 /* CRYPTODEV_FREESESSION (cryptodev_if.m:113-116) */
 void espgpu_freesession(espgpu_ctx *ctx, int32_t session);
 /* CRYPTODEV_PROCESS (cryptodev_if.m:143-147): never blocks.  Stages the
- * request; returns 0, or ERESTART when the staging batch is full (the framework
- * then sets cc_qblocked and requeues, crypto.c:1451-1459).  Malformed requests
- * complete with crp_etype = EINVAL via poll(), as crypto_done would.  `hint`
- * (CRYPTO_HINT_MORE) is accepted and ignored: staged requests launch at
- * espgpu_flush (once per RX burst) or when a staging slot fills. */
+ * request; returns 0, or ERESTART when every staging slot is in flight (the
+ * framework then sets cc_qblocked and requeues, crypto.c:1451-1459).  With
+ * set_tuning "overflow_mb" > 0 such a request is kept in a host overflow
+ * instead (ERESTART only once that many MiB are held), which the next
+ * espgpu_flush moves into the slots as they free: F-Stack runs no
+ * crypto_proc thread to requeue.  A record lying
+ * in one segment of memory registered with espgpu_register_host is not
+ * copied by the CPU: the GPU reads it and writes the results back in place.
+ * Malformed requests complete with crp_etype = EINVAL via poll(), as
+ * crypto_done would.  `hint` (CRYPTO_HINT_MORE) is accepted and ignored:
+ * staged requests launch at espgpu_flush (once per RX burst) or when a
+ * staging slot fills. */
 int  espgpu_process(espgpu_ctx *ctx, const struct espgpu_req *req, int hint);
-/* Launch everything staged so far: H2D, kernels and D2H on three ctx streams
+/* Launch everything staged so far, then move the overflow into the slots
+ * that are free: a small batch runs copy, kernels, copy in order on its
+ * slot's stream; a large one H2D, kernels and D2H on three ctx streams
  * chained by events, so consecutive batches overlap copies with kernels.
- * F-Stack's main_loop calls this once per RX burst (lib/ff_dpdk_if.c:2363). */
+ * Never waits.  F-Stack's main_loop calls this once per RX burst
+ * (lib/ff_dpdk_if.c:2363). */
 int  espgpu_flush(espgpu_ctx *ctx);
 /* Complete finished requests: copies results back into the caller's segments
  * (only for etype 0: EBADMSG leaves the buffer unchanged) and returns up to
  * `max` completions; the shim calls crypto_done() for each. */
 int  espgpu_poll(espgpu_ctx *ctx, struct espgpu_completion *out, int max);
-/* Block until everything flushed has completed (teardown / tests). */
+/* Block until everything staged, flushed or in the overflow has completed
+ * (teardown / tests); the completions wait for espgpu_poll. */
 int  espgpu_drain(espgpu_ctx *ctx);
+/* Register host memory the requests' buffers live in (DPDK mbuf pools:
+ * F-Stack's mbuf data is the mbuf's own hugepage buffer, lib/ff_veth.c:
+ * 367-389; ff_dpdk_register_gpu_mem walks the pools with
+ * rte_mempool_mem_iter).  hipHostRegister maps it
+ * for the device once; process() then stages a record that lies in it by
+ * reference, and the xfer kernel reads it into the device batch and writes
+ * the results back (payload; ICV when encrypting; nothing for a record that
+ * fails) with no CPU copy.  Memory already pinned (hipHostMalloc) is mapped
+ * as is.  Regions must not overlap: EINVAL.  Unregister drains first. */
+int  espgpu_register_host(espgpu_ctx *ctx, void *base, uint64_t len);
+int  espgpu_unregister_host(espgpu_ctx *ctx, void *base);
 int  espgpu_get_stats(espgpu_ctx *ctx, struct espgpu_stats *st);
 
 /* ---- device-resident batch path ----
@@ -304,6 +329,10 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
  *               decrypt (MODE 3) out of place, 1 one fused pass per record
  *               (MODE 0), 0 separate verify / decrypt kernels; others EINVAL;
+ *   "overflow_mb" host overflow for process() while every staging slot is
+ *               in flight, in MiB (0, the default: ERESTART; 0..65536);
+ *   "xfer"      small batches' staging region moved by the xfer kernel (1,
+ *               default) or by hipMemcpyAsync (0);
  *   "gcm_opts" / "eta_opts" measurement knobs that skip work on purpose
  *               (results wrong): only in libespgpu_knobs.so, ENOTSUP in the
  *               product library unless 0.

@@ -80,6 +80,7 @@ gpucrypto_errno(int abi)
 	case ESPGPU_ERESTART: return (ERESTART);     /* -1 */
 	case ESPGPU_EAGAIN:   return (EAGAIN);       /* 35 */
 	case ESPGPU_ENOMEM:   return (ENOMEM);
+	case ESPGPU_ENOBUFS:  return (ENOBUFS);
 	case ESPGPU_ENXIO:    return (ENXIO);
 	case ESPGPU_ENODEV:   return (ENODEV);
 	case ESPGPU_ENOENT:   return (ENOENT);

@@ -28,12 +28,20 @@ static espgpu_ctx *g_ctx;          /* one F-Stack process = one lcore = one ctx 
 /* F-Stack runs no crypto_proc thread (its kproc/kthread stubs never start
  * one, lib/ff_compat.c:156-171), so a request that crypto_dispatch queues on
  * ERESTART (crypto.c:1450-1459) would never be re-dispatched there.  With
- * no-queue set, process() makes room instead of answering ERESTART. */
+ * no-queue set, the engine keeps requests that arrive while every staging
+ * slot is in flight in a host overflow (set_tuning "overflow_mb"), launched
+ * by the next ff_gpucrypto_poll(): process() never waits for the GPU
+ * (cryptodev_if.m:143-147).  Past the overflow's size a request completes
+ * with ENOBUFS: esp_input_cb drops it, as esp_input drops a packet it cannot
+ * get a cryptop for (xform_esp.c:348-354). */
 static int g_noqueue;
+#define FF_GPUCRYPTO_OVERFLOW_MB 256
 
 void ff_gpucrypto_host_set_noqueue(int on)
 {
 	g_noqueue = on;
+	if (g_ctx)
+		espgpu_set_tuning(g_ctx, "overflow_mb", on ? FF_GPUCRYPTO_OVERFLOW_MB : 0);
 }
 
 int ff_gpucrypto_host_init(int gpu)
@@ -49,12 +57,14 @@ int ff_gpucrypto_host_init(int gpu)
  * section 6 with one process per GPU. */
 int ff_gpucrypto_host_init_proc(int proc_id)
 {
-	int n = espgpu_device_count();
+	int n = espgpu_device_count(), e;
 
 	if (n <= 0)
 		return ESPGPU_ENODEV;
-	g_noqueue = 1;
-	return ff_gpucrypto_host_init(proc_id % n);
+	e = ff_gpucrypto_host_init(proc_id % n);
+	if (e == ESPGPU_OK)
+		ff_gpucrypto_host_set_noqueue(1);
+	return e;
 }
 
 /* as ff_gpucrypto_host_init, with explicit staging sizes (batch_records,
@@ -63,6 +73,15 @@ int ff_gpucrypto_host_init_proc(int proc_id)
 int ff_gpucrypto_host_configure(const struct espgpu_config *c)
 {
 	return espgpu_init(c, &g_ctx);
+}
+
+/* Register mbuf memory (one DPDK mempool memory chunk; the patched
+ * ff_dpdk_if.c walks the pktmbuf pools with rte_mempool_mem_iter after
+ * ff_gpucrypto_host_init_proc): records in it are read and written back by
+ * the GPU, with no gather into the staging buffer. */
+int ff_gpucrypto_host_register(void *base, uint64_t len)
+{
+	return g_ctx ? espgpu_register_host(g_ctx, base, len) : ESPGPU_ENXIO;
 }
 
 /* the kernel-domain driver's device_probe: attach only with a GPU context */
@@ -78,6 +97,18 @@ void ff_gpucrypto_host_fini(void)
 		espgpu_fini(g_ctx);
 		g_ctx = NULL;
 	}
+}
+
+/* engine counters (overflow / zero-copy records, ERESTARTs) and knobs, for
+ * the tests and an operator's sysctl-style view */
+int ff_gpucrypto_host_stats(struct espgpu_stats *st)
+{
+	return g_ctx ? espgpu_get_stats(g_ctx, st) : ESPGPU_ENXIO;
+}
+
+int ff_gpucrypto_host_tune(const char *key, int value)
+{
+	return g_ctx ? espgpu_set_tuning(g_ctx, key, value) : ESPGPU_ENXIO;
 }
 
 /* CRYPTODEV_PROBESESSION: -100 (CRYPTODEV_PROBE_HARDWARE) or EINVAL.
@@ -107,13 +138,8 @@ int ff_gpucrypto_host_process(const struct espgpu_req *r, int hint)
 	if (!g_ctx)
 		return ESPGPU_ENXIO;
 	e = espgpu_process(g_ctx, r, hint);
-	if (e == ESPGPU_ERESTART && g_noqueue) {
-		/* wait for the staged batches (their completions go out with the
-		 * next ff_gpucrypto_poll()), then stage this request */
-		e = espgpu_drain(g_ctx);
-		if (e == ESPGPU_OK)
-			e = espgpu_process(g_ctx, r, hint);
-	}
+	if (e == ESPGPU_ERESTART && g_noqueue)
+		e = ESPGPU_ENOBUFS;         /* overflow full: the driver completes it as a drop */
 	return e;
 }
 
@@ -132,6 +158,9 @@ int ff_gpucrypto_poll(void)
 				ff_gpucrypto_done(c[i].opaque, c[i].etype);
 		total += n;
 	}
+	/* slots the poll retired take the overflow now, not one loop later */
+	if (total && !blocked)
+		blocked = espgpu_flush(g_ctx);
 	if (total && ff_gpucrypto_unblock)
 		ff_gpucrypto_unblock();     /* crypto_unblock(id, CRYPTO_SYMQ), crypto.c:1191 */
 	return blocked ? -blocked : total;

@@ -30,6 +30,7 @@
 #define EINVAL      22
 #define EAGAIN      35
 #define EOPNOTSUPP  45
+#define ENOBUFS     55
 #define EBADMSG     89
 #define ERESTART    (-1)
 

@@ -55,6 +55,7 @@ int main(void)
 	CHECK(gpucrypto_errno(ESPGPU_EAGAIN) == 35);
 	CHECK(gpucrypto_errno(ESPGPU_EINVAL) == 22);
 	CHECK(gpucrypto_errno(ESPGPU_ENOTSUP) == 45);
+	CHECK(gpucrypto_errno(ESPGPU_ENOBUFS) == 55);
 	CHECK(gpucrypto_errno(12345) == EIO);
 
 	CHECK(kmock_attach(&ff_gpucrypto_kmock) == 0);

@@ -105,4 +105,8 @@ def test_fstack_patch_applies_and_fixes_the_ipsec_build(tmp_path):
     # the GPU context exists before ff_freebsd_init() attaches the drivers
     assert (init.index("ret = ff_dpdk_init(") < init.index("ff_gpucrypto_host_init_proc(ff_global_cfg")
             < init.index("ret = ff_freebsd_init();"))
+    # the mbuf pools (made by ff_dpdk_init) are mapped for the GPU once the context exists
+    assert (init.index("ff_gpucrypto_host_init_proc(ff_global_cfg") < init.index("ff_dpdk_register_gpu_mem()")
+            < init.index("ret = ff_freebsd_init();"))
+    assert "rte_mempool_mem_iter(pktmbuf_pool[i], ff_gpucrypto_mem_cb" in loop
     assert (lib / "ff_newbus.c").exists()

@@ -1,0 +1,279 @@
+"""The opencrypto burst path without CPU copies or blocking (F-Stack mode):
+
+* registered host memory (espgpu_register_host, hipHostRegister: DPDK mbuf
+  pages in F-Stack, lib/ff_veth.c:367-389): records that lie in it are read
+  into the device batch and their results written back by the xfer kernel,
+  at any byte alignment (ESP sits 2 mod 4 in an mbuf), mixed in one batch
+  with records from unregistered buffers (gathered as before), every
+  session kind, small batches (one slot stream; staging region by the xfer
+  kernel or hipMemcpyAsync) and large ones (three streams);
+* the host overflow (set_tuning "overflow_mb"): process() keeps accepting
+  while every staging slot is in flight, flush moves the overflow into the
+  slots as they free, ERESTART only past the cap.
+
+Every result is checked against the oracle: ciphertext and ICV bytes for
+esp_output, plaintext for esp_input, EBADMSG with the buffer untouched for a
+tampered record (cryptosoft's swcr_gcm / swcr_eta semantics,
+cryptosoft.c:465-645, :874-888)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import EtaSA, GcmSA, build_records
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _driver(**kw):
+    from espgpu.opencrypto import GpuCryptoDriver
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible HIP device")
+    return GpuCryptoDriver(**kw)
+
+
+def _sas(rng):
+    return [GcmSA(rng, 16), GcmSA(rng, 32, esn=True, mlen=12), EtaSA(rng, 32),
+            EtaSA(rng, 16, ctr=True, sha=256, esn=True), EtaSA(rng, null=True, sha=1),
+            EtaSA(rng, 16, noauth=True), EtaSA(rng, 24, sha=512)]
+
+
+def _cts(rng, sas, idx):
+    cbc = rng.choice([16, 48, 208, 1440], len(idx))
+    free = rng.choice([4, 12, 100, 1448], len(idx))
+    return np.where([isinstance(sas[i], EtaSA) and not sas[i].ctr and not sas[i].null for i in idx], cbc, free)
+
+
+class _Layout:
+    """Records copied out of build_records' arena to their packet positions:
+    registered ones into `reg` at every byte alignment behind a `skip`-byte
+    outer header, the rest into their own bytearrays."""
+
+    def __init__(self, rng, descs, n, reg, frac_reg=0.75, skip=20):
+        self.skip = skip
+        self.where = []            # (registered?, buffer offset or bytearray)
+        pos = 64
+        for i in range(n):
+            L = int(descs["len"][i])
+            if rng.random() < frac_reg:
+                base = pos + skip + (i % 16)       # record start: all 16 residues
+                self.where.append((True, base))
+                pos = base + L + 40
+            else:
+                self.where.append((False, bytearray(skip + L)))
+        assert pos < len(reg)
+        self.reg, self.descs = reg, descs
+
+    def pkt(self, i):
+        r, w = self.where[i]
+        L = int(self.descs["len"][i])
+        return self.reg[w - self.skip:w + L] if r else w
+
+    def put(self, i, arena):
+        o, L = int(self.descs["off4"][i]) * 4, int(self.descs["len"][i])
+        p = self.pkt(i)
+        src = arena[o:o + L]
+        p[self.skip:self.skip + L] = src if isinstance(p, np.ndarray) else src.tobytes()
+
+    def get(self, i):
+        return bytes(self.pkt(i)[self.skip:])
+
+
+def _run(fw, crps):
+    for c in crps:
+        assert fw.crypto_dispatch(c) == 0
+    fw.crypto_drain()
+
+
+@pytest.mark.parametrize("xfer", [1, 0])
+@pytest.mark.parametrize("n", [60, 500])
+def test_registered_memory_zero_copy_vs_oracle(xfer, n):
+    """n = 60: one small batch (<= 128 KiB, the slot's own stream); 500: a
+    large batch (three streams, zero-copy records moved on the compute
+    stream).  Encrypt, then decrypt with tampered records."""
+    from espgpu.esp import esp_input_crp, esp_output_crp
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=16)
+    try:
+        assert drv.set_tuning("xfer", xfer) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2100 + n + xfer)
+        sas = _sas(rng)
+        ses = []
+        for s in sas:
+            err, cs = fw.crypto_newsession(s.esp_sa().csp())
+            assert err == 0
+            ses.append(cs)
+        idx = rng.integers(0, len(sas), n)
+        eh = rng.integers(0, 2**32, n, dtype=np.uint32)
+        plain, ct, descs, eh = build_records(rng, sas, idx, _cts(rng, sas, idx), esn_hi=eh)
+        reg = np.zeros(1 << 20, dtype=np.uint8)
+        drv.register_host(reg)
+        lay = _Layout(rng, descs, n, reg)
+        nreg = sum(r for r, _ in lay.where)
+        assert 0 < nreg < n
+        # esp_output
+        for i in range(n):
+            lay.put(i, plain)
+        z0 = drv.stats()["zerocopy"]
+        crps = [esp_output_crp(fw, ses[idx[i]], sas[idx[i]].esp_sa(), lay.pkt(i), lay.skip,
+                               esn_hi=int(eh[i])) for i in range(n)]
+        _run(fw, crps)
+        assert drv.stats()["zerocopy"] - z0 == nreg
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert crps[i].crp_etype == 0
+            assert lay.get(i) == bytes(ct[o:o + L]), (i, lay.where[i][0])
+        # esp_input, some records tampered
+        bad = set(int(i) for i in rng.choice(n, max(3, n // 10), replace=False))
+        before = {}
+        for i in range(n):
+            lay.put(i, ct)
+            if i in bad:
+                p = lay.pkt(i)
+                p[lay.skip + int(descs["len"][i]) - 1 - int(rng.integers(0, 4))] ^= 0x10
+                before[i] = lay.get(i)
+        crps = [esp_input_crp(fw, ses[idx[i]], sas[idx[i]].esp_sa(), lay.pkt(i), lay.skip,
+                              esn_hi=int(eh[i])) for i in range(n)]
+        _run(fw, crps)
+        for i in range(n):
+            sa = sas[idx[i]]
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            got = lay.get(i)
+            if i in bad and sa.mlen:
+                assert crps[i].crp_etype == O.EBADMSG, i
+                assert got == before[i], i                     # untouched
+            elif i not in bad:
+                assert crps[i].crp_etype == 0, i
+                h, a = sa.hlen, sa.mlen
+                assert got[h:L - a] == bytes(plain[o + h:o + L - a]), (i, lay.where[i][0])
+                assert got[:h] == bytes(ct[o:o + h]) and got[L - a:] == bytes(ct[o + L - a:o + L])
+        # the bytes around each registered record are never written
+        for i in range(n):
+            r, w = lay.where[i]
+            if r:
+                L = int(descs["len"][i])
+                assert not reg[w - lay.skip:w].any() and not reg[w + L:w + L + 16].any(), i
+        for s in ses:
+            fw.crypto_freesession(s)
+        drv.unregister_host(reg)
+    finally:
+        drv.close()
+
+
+def test_unregister_falls_back_to_gather():
+    from espgpu.esp import esp_input_crp
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=4)
+    try:
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2200)
+        sas = [GcmSA(rng, 16)]
+        err, cs = fw.crypto_newsession(sas[0].esp_sa().csp())
+        assert err == 0
+        n = 24
+        idx = np.zeros(n, dtype=np.int64)
+        plain, ct, descs, eh = build_records(rng, sas, idx, np.full(n, 1448))
+        reg = np.zeros(1 << 17, dtype=np.uint8)
+        drv.register_host(reg)
+        with pytest.raises(RuntimeError):
+            drv.register_host(reg[100:200])                  # overlaps: EINVAL
+        lay = _Layout(rng, descs, n, reg, frac_reg=1.0, skip=34)
+        for rnd in range(2):
+            for i in range(n):
+                lay.put(i, ct)
+            z0 = drv.stats()["zerocopy"]
+            crps = [esp_input_crp(fw, cs, sas[0].esp_sa(), lay.pkt(i), lay.skip) for i in range(n)]
+            _run(fw, crps)
+            assert drv.stats()["zerocopy"] - z0 == (n if rnd == 0 else 0)
+            for i in range(n):
+                o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+                assert crps[i].crp_etype == 0
+                assert lay.get(i)[16:L - 16] == bytes(plain[o + 16:o + L - 16])
+            if rnd == 0:
+                drv.unregister_host(reg)
+        fw.crypto_freesession(cs)
+    finally:
+        drv.close()
+
+
+def _gcm_reqs(rng, n, ct_len):
+    sas = [GcmSA(rng, 16), GcmSA(rng, 16)]
+    idx = rng.integers(0, 2, n)
+    plain, ct, descs, eh = build_records(rng, sas, idx, np.full(n, ct_len))
+    return sas, idx, plain, ct, descs
+
+
+def test_overflow_keeps_accepting_while_slots_in_flight():
+    """4-record slots, two of them: 40 requests in one burst never see
+    ERESTART (32 wait in the overflow); flush + poll, as F-Stack's main_loop
+    hook does, completes all of them in order of arrival, bit-exact."""
+    from espgpu.esp import esp_input_crp
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=4, batch_records=4, nbatches=2)
+    try:
+        assert drv.set_tuning("overflow_mb", 1) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2300)
+        n = 40
+        sas, idx, plain, ct, descs = _gcm_reqs(rng, n, 1448)
+        ses = [fw.crypto_newsession(s.esp_sa().csp())[1] for s in sas]
+        pkts = []
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            pkts.append(bytearray(bytes(ct[o:o + L])))
+        crps = [esp_input_crp(fw, ses[idx[i]], sas[idx[i]].esp_sa(), pkts[i], 0) for i in range(n)]
+        s0 = drv.stats()
+        for c in crps:
+            assert drv.process(c) == 0                     # never ERESTART
+        s1 = drv.stats()
+        assert s1["overflow"] - s0["overflow"] >= n - 8 and s1["erestart"] == s0["erestart"]
+        order, spins = [], 0
+        while len(order) < n:
+            drv.flush()
+            order += [id(c) for c in drv.poll()]
+            spins += 1
+            assert spins < 10**6
+        assert order == [id(c) for c in crps]              # arrival order
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert crps[i].crp_etype == 0
+            assert bytes(pkts[i][16:L - 16]) == bytes(plain[o + 16:o + L - 16])
+        assert drv.set_tuning("overflow_mb", -1) == 22
+    finally:
+        drv.close()
+
+
+def test_overflow_cap_then_erestart():
+    """1 MiB of overflow holds ~115 9000-B records: beyond it process()
+    answers ERESTART; the framework requeues those (cc_qblocked) and every
+    request completes bit-exact."""
+    from espgpu.esp import esp_output_crp
+    from espgpu.opencrypto import ERESTART, CryptoFramework
+    drv = _driver(max_sessions=4, batch_records=4, nbatches=2)
+    try:
+        assert drv.set_tuning("overflow_mb", 1) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2400)
+        n = 200
+        sas, idx, plain, ct, descs = _gcm_reqs(rng, n, 8948)
+        ses = [fw.crypto_newsession(s.esp_sa().csp())[1] for s in sas]
+        pkts = []
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            pkts.append(bytearray(bytes(plain[o:o + L])))
+        crps = [esp_output_crp(fw, ses[idx[i]], sas[idx[i]].esp_sa(), pkts[i], 0) for i in range(n)]
+        rcs = [drv.process(c) for c in crps]
+        nre = rcs.count(ERESTART)
+        assert set(rcs) <= {0, ERESTART} and 60 < nre < n - 100
+        first = rcs.index(ERESTART)
+        assert all(r == ERESTART for r in rcs[first:])      # the cap holds once reached
+        fw._blocked = [crps[i] for i in range(first, n)]    # requeued as crypto_dispatch would
+        fw.crypto_drain()
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert crps[i].crp_etype == 0
+            assert bytes(pkts[i]) == bytes(ct[o:o + L])
+    finally:
+        drv.close()

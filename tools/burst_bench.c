@@ -6,14 +6,29 @@
  *
  *   make -C tools burst_bench && ./tools/burst_bench [burst ...]
  *
- * For each burst size B (default 32 = MAX_PKT_BURST, lib/ff_dpdk_if.c):
- *   latency   B decrypt requests staged, flushed, polled until all B have
- *             completed (one burst in flight); median / p99 over 2000 bursts
- *   pipelined bursts issued back to back, up to `nbatches` (2) in flight,
- *             completions polled between them: sustained records/s
- * Records: ESP AES-128-GCM, 1500-byte packets (1480-byte ESP records, one
- * contiguous buffer each), encrypted by the engine first, restored from a
- * copy before every decrypt so every tag verifies.  One JSON line per B.
+ * For each burst size B (default 32 = MAX_PKT_BURST, lib/ff_dpdk_if.c) and
+ * each way the records reach the GPU:
+ *   mode   "gather"      records in ordinary (pageable) memory: process()
+ *                        copies them into the pinned staging buffer;
+ *          "registered"  the record buffers registered once
+ *                        (espgpu_register_host, as F-Stack registers its mbuf
+ *                        pools): the GPU reads them and writes the results
+ *                        back, no CPU copy;
+ *   xfer   1 = a small batch's staging region moved by the xfer kernel,
+ *          0 = by hipMemcpyAsync (set_tuning "xfer");
+ * it reports
+ *   latency     B decrypt requests staged, flushed, polled until all B have
+ *               completed (one burst in flight); median / p99 over the bursts
+ *   pipelined   bursts issued back to back, completions polled in between,
+ *               ERESTART answered by flush + poll + retry (overflow off)
+ *   fstack      the F-Stack main_loop shape: per iteration stage B, flush,
+ *               poll once, never wait; process() never sees ERESTART (host
+ *               overflow on, set_tuning "overflow_mb")
+ * Records: ESP AES-128-GCM, 1500-byte packets (1480-byte ESP records), each
+ * in its own 1536-byte buffer at offset 162 = DPDK headroom 128 + Ethernet 14
+ * + IPv4 20 (2 mod 4, where an mbuf puts them); encrypted by the engine first,
+ * restored from a copy before every decrypt so every tag verifies.  One JSON
+ * line per (B, mode, xfer).
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -24,9 +39,16 @@
 #include "espgpu.h"
 
 #define REC 1480
+#define STRIDE 1536
+#define OFF 162
+#define RING 16                       /* bursts of buffers in the ring */
 #define CK(x) do { int e_ = (x); if (e_) { fprintf(stderr, "%s -> %d (%s)\n", #x, e_, espgpu_last_error(ctx)); exit(1); } } while (0)
 
 static espgpu_ctx *ctx;
+static uint8_t *bufs, *ct;
+static struct espgpu_req *req;
+static struct espgpu_seg *seg;
+static int pool;
 
 static double now_us(void)
 {
@@ -41,16 +63,18 @@ static int cmp_d(const void *a, const void *b)
 	return x < y ? -1 : x > y;
 }
 
-static void make_req(struct espgpu_req *r, struct espgpu_seg *seg, uint8_t *buf, int32_t sid, int enc,
-                     const uint8_t salt[4], void *opaque)
+static uint8_t *rec_of(int i) { return bufs + (size_t)i * STRIDE + OFF; }
+
+static void make_req(struct espgpu_req *r, struct espgpu_seg *sg, uint8_t *buf, int32_t sid, int enc,
+                     const uint8_t salt[4])
 {
 	memset(r, 0, sizeof(*r));
-	seg->base = buf;
-	seg->len = REC;
+	sg->base = buf;
+	sg->len = REC;
 	r->session = sid;
 	r->crp_op = enc ? ESPGPU_CRYPTO_OP_ENCRYPT : ESPGPU_CRYPTO_OP_VERIFY_DIGEST;
 	r->crp_flags = ESPGPU_CRYPTO_F_IV_SEPARATE;
-	r->segs = seg;
+	r->segs = sg;
 	r->nsegs = 1;
 	r->crp_aad_start = 0;
 	r->crp_aad_length = 8;
@@ -59,27 +83,74 @@ static void make_req(struct espgpu_req *r, struct espgpu_seg *seg, uint8_t *buf,
 	r->crp_digest_start = REC - 16;
 	memcpy(r->crp_iv, salt, 4);
 	memcpy(r->crp_iv + 4, buf + 8, 8);
-	r->opaque = opaque;
 }
 
-/* stage n requests (retrying ERESTART after a poll), return completions seen */
-static int submit(struct espgpu_req *r, int n, int *done, int *bad)
+static int poll_some(int *bad)
 {
-	struct espgpu_completion c[1024];
+	struct espgpu_completion c[4096];
+	int k = espgpu_poll(ctx, c, 4096);
+	for (int j = 0; j < k; j++) *bad += c[j].etype != 0;
+	return k;
+}
+
+/* stage n requests (retrying ERESTART after a flush + poll), return completions seen */
+static void submit(struct espgpu_req *r, int n, int *done, int *bad)
+{
 	for (int i = 0; i < n; i++) {
 		int e;
 		while ((e = espgpu_process(ctx, &r[i], 0)) == ESPGPU_ERESTART) {
 			espgpu_flush(ctx);
-			int k = espgpu_poll(ctx, c, 1024);
-			for (int j = 0; j < k; j++) *bad += c[j].etype != 0;
-			*done += k;
+			*done += poll_some(bad);
 		}
 		if (e) {
 			fprintf(stderr, "process: %d\n", e);
 			exit(1);
 		}
 	}
-	return 0;
+}
+
+static void restore(int base, int B)
+{
+	for (int i = base; i < base + B; i++)
+		memcpy(rec_of(i), ct + (size_t)i * REC, REC);
+}
+
+/* bursts back to back; the ring of RING bursts is only reused once its
+ * results are back.  fstack: process() must never answer ERESTART. */
+static double pipelined(int B, int iters, int fstack, int *bad, double *worst_process_us)
+{
+	int done = 0;
+	*worst_process_us = 0;
+	double t0 = now_us();
+	for (int it = 0; it < iters; it++) {
+		const int base = (it % RING) * B;
+		while (done < (it - (RING - 1)) * B) {
+			espgpu_flush(ctx);
+			done += poll_some(bad);
+		}
+		restore(base, B);
+		if (fstack) {
+			for (int i = 0; i < B; i++) {
+				double p0 = now_us();
+				int e = espgpu_process(ctx, &req[base + i], 0);
+				double dp = now_us() - p0;
+				*worst_process_us = dp > *worst_process_us ? dp : *worst_process_us;
+				if (e) {
+					fprintf(stderr, "fstack mode: process -> %d\n", e);
+					exit(1);
+				}
+			}
+		} else {
+			submit(req + base, B, &done, bad);
+		}
+		espgpu_flush(ctx);
+		done += poll_some(bad);
+	}
+	while (done < iters * B) {
+		espgpu_flush(ctx);
+		done += poll_some(bad);
+	}
+	return now_us() - t0;
 }
 
 int main(int argc, char **argv)
@@ -105,83 +176,79 @@ int main(int argc, char **argv)
 	int32_t sid;
 	CK(espgpu_newsession(ctx, &p, &sid));
 
-	const int pool = maxb * 4;          /* distinct buffers so bursts in flight do not alias */
-	uint8_t *bufs = malloc((size_t)pool * REC), *ct = malloc((size_t)pool * REC);
-	struct espgpu_req *req = malloc(sizeof(*req) * pool);
-	struct espgpu_seg *seg = malloc(sizeof(*seg) * pool);
+	pool = maxb * RING;
+	const size_t bytes = (size_t)pool * STRIDE;
+	if (posix_memalign((void **)&bufs, 4096, bytes)) return 1;
+	ct = malloc((size_t)pool * REC);
+	req = malloc(sizeof(*req) * pool);
+	seg = malloc(sizeof(*seg) * pool);
 	srand(3);
-	for (size_t i = 0; i < (size_t)pool * REC; i++) bufs[i] = (uint8_t)rand();
+	for (size_t i = 0; i < bytes; i++) bufs[i] = (uint8_t)rand();
 	int done = 0, bad = 0;
 	for (int i = 0; i < pool; i++) {
-		memset(bufs + (size_t)i * REC + REC - 16, 0, 16);
-		make_req(&req[i], &seg[i], bufs + (size_t)i * REC, sid, 1, salt, NULL);
+		memset(rec_of(i) + REC - 16, 0, 16);
+		make_req(&req[i], &seg[i], rec_of(i), sid, 1, salt);
 	}
 	submit(req, pool, &done, &bad);
 	CK(espgpu_drain(ctx));
 	struct espgpu_completion c[4096];
 	while (espgpu_poll(ctx, c, 4096) > 0) {}
-	memcpy(ct, bufs, (size_t)pool * REC);
-	for (int i = 0; i < pool; i++)
-		make_req(&req[i], &seg[i], bufs + (size_t)i * REC, sid, 0, salt, NULL);
-
-	for (int bi = 0; bi < nb; bi++) {
-		const int B = bursts[bi];
-		const int iters = B <= 64 ? 2000 : (B <= 512 ? 400 : 60);
-		double *lat = malloc(sizeof(double) * iters);
-		bad = 0;
-		/* latency: one burst in flight */
-		for (int it = -20; it < iters; it++) {
-			const int base = (it & 3) * B;
-			memcpy(bufs + (size_t)base * REC, ct + (size_t)base * REC, (size_t)B * REC);
-			done = 0;
-			double t0 = now_us();
-			submit(req + base, B, &done, &bad);
-			espgpu_flush(ctx);
-			while (done < B) {
-				int k = espgpu_poll(ctx, c, 4096);
-				for (int j = 0; j < k; j++) bad += c[j].etype != 0;
-				done += k;
-			}
-			if (it >= 0) lat[it] = now_us() - t0;
-		}
-		const int bad_latency = bad;
-		qsort(lat, iters, sizeof(double), cmp_d);
-		const double med = lat[iters / 2], p99 = lat[(int)(iters * 0.99)];
-		/* pipelined: bursts back to back, completions polled in between */
-		const int total_bursts = iters;
-		done = 0;
-		double t0 = now_us();
-		for (int it = 0; it < total_bursts; it++) {
-			const int base = (it & 3) * B;
-			/* a fresh burst of ciphertext arrives (inside the timed loop: the
-			 * 4-burst buffer ring is only reused after its results are back) */
-			while (done < (it - 3) * B) {
-				int k = espgpu_poll(ctx, c, 4096);
-				for (int j = 0; j < k; j++) bad += c[j].etype != 0;
-				done += k;
-			}
-			memcpy(bufs + (size_t)base * REC, ct + (size_t)base * REC, (size_t)B * REC);
-			submit(req + base, B, &done, &bad);
-			espgpu_flush(ctx);
-			int k = espgpu_poll(ctx, c, 4096);
-			for (int j = 0; j < k; j++) bad += c[j].etype != 0;
-			done += k;
-		}
-		while (done < total_bursts * B) {
-			espgpu_flush(ctx);
-			int k = espgpu_poll(ctx, c, 4096);
-			for (int j = 0; j < k; j++) bad += c[j].etype != 0;
-			done += k;
-		}
-		const double dt = now_us() - t0;
-		printf("{\"burst\": %d, \"record_bytes\": %d, \"latency_us_median\": %.1f, \"latency_us_p99\": %.1f, "
-		       "\"latency_records_per_s\": %.0f, \"pipelined_records_per_s\": %.0f, \"pipelined_GBps\": %.3f, "
-		       "\"iters\": %d, \"auth_fail\": [%d, %d]}\n",
-		       B, REC, med, p99, B / med * 1e6, total_bursts * (double)B / dt * 1e6,
-		       total_bursts * (double)B * REC / dt / 1e3, iters, bad_latency, bad - bad_latency);
-		fflush(stdout);
-		free(lat);
+	for (int i = 0; i < pool; i++) {
+		memcpy(ct + (size_t)i * REC, rec_of(i), REC);
+		make_req(&req[i], &seg[i], rec_of(i), sid, 0, salt);
 	}
+
+	for (int mode = 0; mode < 2; mode++) {
+		if (mode == 1) CK(espgpu_register_host(ctx, bufs, bytes));
+		for (int xfer = 1; xfer >= 0; xfer--) {
+			CK(espgpu_set_tuning(ctx, "xfer", xfer));
+			for (int bi = 0; bi < nb; bi++) {
+				const int B = bursts[bi];
+				const int iters = B <= 64 ? 2000 : (B <= 512 ? 400 : 60);
+				double *lat = malloc(sizeof(double) * iters);
+				struct espgpu_stats s0, s1;
+				CK(espgpu_get_stats(ctx, &s0));
+				bad = 0;
+				/* latency: one burst in flight */
+				for (int it = -20; it < iters; it++) {
+					const int base = ((it + 20) % RING) * B;
+					restore(base, B);
+					done = 0;
+					double t0 = now_us();
+					submit(req + base, B, &done, &bad);
+					espgpu_flush(ctx);
+					while (done < B) done += poll_some(&bad);
+					if (it >= 0) lat[it] = now_us() - t0;
+				}
+				const int bad_latency = bad;
+				qsort(lat, iters, sizeof(double), cmp_d);
+				const double med = lat[iters / 2], p99 = lat[(int)(iters * 0.99)];
+				double wp;
+				CK(espgpu_set_tuning(ctx, "overflow_mb", 0));
+				const double dt = pipelined(B, iters, 0, &bad, &wp);
+				CK(espgpu_set_tuning(ctx, "overflow_mb", 256));
+				double wf;
+				const double df = pipelined(B, iters, 1, &bad, &wf);
+				CK(espgpu_set_tuning(ctx, "overflow_mb", 0));
+				CK(espgpu_get_stats(ctx, &s1));
+				printf("{\"burst\": %d, \"mode\": \"%s\", \"xfer\": %d, \"record_bytes\": %d, "
+				       "\"latency_us_median\": %.1f, \"latency_us_p99\": %.1f, \"latency_records_per_s\": %.0f, "
+				       "\"pipelined_records_per_s\": %.0f, \"pipelined_GBps\": %.3f, "
+				       "\"fstack_records_per_s\": %.0f, \"fstack_GBps\": %.3f, \"fstack_max_process_us\": %.1f, "
+				       "\"batches\": %llu, \"overflow\": %llu, \"zerocopy\": %llu, "
+				       "\"iters\": %d, \"auth_fail\": [%d, %d]}\n",
+				       B, mode ? "registered" : "gather", xfer, REC, med, p99, B / med * 1e6,
+				       iters * (double)B / dt * 1e6, iters * (double)B * REC / dt / 1e3,
+				       iters * (double)B / df * 1e6, iters * (double)B * REC / df / 1e3, wf,
+				       (unsigned long long)(s1.batches - s0.batches),
+				       (unsigned long long)(s1.overflow - s0.overflow),
+				       (unsigned long long)(s1.zerocopy - s0.zerocopy), iters, bad_latency, bad - bad_latency);
+				fflush(stdout);
+				free(lat);
+			}
+		}
+	}
+	CK(espgpu_unregister_host(ctx, bufs));
 	espgpu_freesession(ctx, sid);
 	espgpu_fini(ctx);
 	return 0;
