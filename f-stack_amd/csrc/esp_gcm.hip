@@ -46,6 +46,20 @@
 
 #include "espgpu_internal.h"
 
+// Experiment switches (tools/variant.sh builds; defaults are the product)
+#ifndef GCM_STORE_LATE
+#define GCM_STORE_LATE 0
+#endif
+#ifndef GCM_WG
+#define GCM_WG 1024
+#endif
+#ifndef GCM_CTR_SINGLE
+#define GCM_CTR_SINGLE 0
+#endif
+#ifndef GCM_SPLIT_WPE
+#define GCM_SPLIT_WPE 4
+#endif
+
 namespace espgpu {
 
 namespace {
@@ -488,14 +502,26 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
             Ba = xor4(Ca, ka);
             Bb = xor4(Cb, kb);
           }
+#if !GCM_STORE_LATE
           if (MODE != 2 && valid && !(gopts() & 9)) {
             st16(orec + 16 * i, MODE == 1 ? Ba : xor4(Ca, ka));
             st16(orec + 16 * ib, MODE == 1 ? Bb : xor4(Cb, kb));
           }
+#else
+          const uint4 Oa = MODE == 1 ? Ba : xor4(Ca, ka), Ob = MODE == 1 ? Bb : xor4(Cb, kb);
+#endif
           if (gopts() & 2)
             Y = xor4(xor4(Y, Ba), Bb);
           else
             Y = xor4(gf_mul8(xor4(gf_mul8(Y, lds, gl), Ba), lds, gl), Bb);
+#if GCM_STORE_LATE
+          // stores after the GHASH: its wait for this pair's ciphertext does
+          // not also wait for the stores (vmcnt counts both, in order)
+          if (MODE != 2 && valid && !(gopts() & 9)) {
+            st16(orec + 16 * i, Oa);
+            st16(orec + 16 * ib, Ob);
+          }
+#endif
           m += 2;
           continue;
         }
@@ -607,6 +633,281 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
+// ---- split design: a CTR pass and a GHASH / tag pass --------------------------
+// The fused kernel above walks each record with S = 4 lanes (the GHASH Horner
+// chain needs few lanes per record), so 256 records per CU are in flight and
+// every store straddles lines.  The split design runs the two halves of GCM
+// with the mapping each one wants:
+//  * ctr pass: AES-CTR only, kCtrLanes = 16 lanes per record (4 records per
+//    wave, 64 per CU), each lane two counter blocks per step; 256-byte
+//    contiguous loads and stores per record per instruction.  It also writes
+//    E_K(J0) for the tag pass (p.ej0[record]) and the fused trailer word.
+//  * tag pass: GHASH only, S = 4 lanes per record as in the fused kernel, with
+//    the 8-bit H^4 table the only LDS table; T = GHASH ^ E_K(J0) from p.ej0.
+// decrypt out of place: ctr (DIR 0) then tag (verify: status; a failed
+// record's trailer word is zeroed); encrypt: ctr (DIR 1, in place) then tag
+// (writes the ICV); decrypt in place, verify first: ctr (DIR 3: E_K(J0)
+// only), tag, then ctr (DIR 2: only records whose status is 0).
+constexpr int kCtrLanes = 16;
+
+template <int DIR>
+__device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
+                                          uint32_t sa, uint32_t mlen, int nr, rkptr rk) {
+  constexpr int S = kCtrLanes;
+  const int lane = threadIdx.x & 63;
+  const int l = lane & (S - 1);
+  const uint32_t slot = (uint32_t)(lane & 31) * 4;        // T-table at LDS offset 0
+  int valid = 0, ct_len = 0, nct = 0, K = 0;
+  uint8_t *rec = p.arena;
+  uint32_t s0c = 0, s1c = 0, s2c = 0;
+  if (have) {
+    const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+    const uint32_t len = dv.y & 0xffffu;
+    ct_len = (int)len - 16 - (int)mlen;
+    valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
+    if (DIR == 2 && valid) valid = p.status[di] == ESPGPU_OK;
+    if (valid) {
+      rec = p.arena + (size_t)dv.x * 4;
+      const uint4 h = ld16(rec);
+      nct = (ct_len + 15) >> 4;
+      K = DIR == 3 ? 1 : (nct + S) / S;                    // J0 + nct blocks over S lanes
+      s0c = bswap32(dv.w) ^ rk[0];
+      s1c = bswap32(h.z) ^ rk[1];
+      s2c = bswap32(h.w) ^ rk[2];
+    }
+  }
+  int Kw = K;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Kw = max(Kw, __shfl_xor(Kw, o));
+  if (Kw == 0) return;
+  const bool want_trl = (DIR == 0 || DIR == 2) && p.trailer != nullptr;
+  uint8_t *orec = DIR == 0 ? p.out - p.arena + rec : rec;
+  const uint32_t rk3 = rk[3];
+  CtrCache cc;
+  cc.hi = -1;
+  // block i of the lane: -1 = J0 (counter 1), CT block i has counter i + 2
+  auto emit = [&](int i, bool loaded, uint4 C, uint4 ks) {
+    if (!valid) return;
+    if (i == -1) {
+      if (DIR != 2) p.ej0[di] = ks;
+      return;
+    }
+    if (!loaded) return;
+    const int rem = ct_len - 16 * i;
+    const uint4 o = xor4(C, ks);
+    st_partial(orec + 16 + 16 * i, o, rem);
+    if (want_trl && i == nct - 1)
+      p.trailer[di] = esp_trailer_word(rem >= 16 ? o.w : (rem > 8 ? o.z : (rem > 4 ? o.y : o.x)),
+                                       (uint32_t)ct_len);
+  };
+  for (int k = 0; k < Kw; k += 2) {
+    const int ia = l - 1 + S * k, ib = ia + S;
+    const bool two = k + 1 < Kw;                           // wave-uniform
+    const bool la = DIR != 3 && valid && ia >= 0 && ia < nct;
+    const bool lb = DIR != 3 && valid && two && ib < nct;
+    uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+    if (la) Ca = ld16(rec + 16 + 16 * ia);
+    if (lb) Cb = ld16(rec + 16 + 16 * ib);
+    const uint32_t ca = (uint32_t)(ia + 2), cb = (uint32_t)(ib + 2);
+    if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
+    uint4 ka, kb = make_uint4(0, 0, 0, 0);
+    if (!GCM_CTR_SINGLE && two && __all((int)(cb >> 8) == cc.hi)) {
+      aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+    } else {
+      ka = aes_ctr(cc, ca, rk3, nr, rk, lds, slot);
+      if (two) {
+        if ((int)(cb >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(cb >> 8), rk, lds, slot);
+        kb = aes_ctr(cc, cb, rk3, nr, rk, lds, slot);
+      }
+    }
+    emit(ia, la, Ca, ka);
+    if (two) emit(ib, lb, Cb, kb);
+  }
+}
+
+template <int DIR, int S>
+__device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
+                                          uint32_t sa, uint32_t sa_flags, uint32_t mlen) {
+  const int lane = threadIdx.x & 63;
+  const int l = lane & (S - 1);
+  const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
+  const GhLane gl = gh_lane(lane);
+  int valid = 0, ct_len = 0, nct = 0, N = 0, M = 0, pad = 0;
+  uint8_t *rec = p.arena;
+  uint32_t len = 0, spi = 0, sn = 0, esnh = 0;
+  if (have) {
+    const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+    len = dv.y & 0xffffu;
+    ct_len = (int)len - 16 - (int)mlen;
+    valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
+    if (valid) {
+      rec = p.arena + (size_t)dv.x * 4;
+      const uint4 h = ld16(rec);
+      spi = h.x;
+      sn = h.y;
+      esnh = bswap32(dv.z);
+      nct = (ct_len + 15) >> 4;
+      N = nct + 2;
+      M = (N + S - 1) / S;
+      pad = S * M - N;
+    }
+  }
+  int Mw = M;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Mw = max(Mw, __shfl_xor(Mw, o));
+  const bool want_trl = DIR == 0 && p.trailer != nullptr;
+  if (Mw == 0) {
+    if (have && l == 0 && !valid) {
+      p.status[di] = ESPGPU_EINVAL;
+      if (want_trl) p.trailer[di] = 0;
+    }
+    return;
+  }
+  // GHASH input block i: 0 = AAD, 1..nct = ciphertext, N-1 = lengths, < 0 = front padding
+  auto blk = [&](int i, bool loaded, uint4 C) -> uint4 {
+    if (loaded) return mask_block(C, ct_len - 16 * (i - 1));
+    if (valid && i == 0) return sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0);
+    if (valid && i == N - 1) return make_uint4(0, bswap32(sep ? 96u : 64u), 0, bswap32((uint32_t)ct_len * 8));
+    return make_uint4(0, 0, 0, 0);
+  };
+  uint4 Y = make_uint4(0, 0, 0, 0);
+  for (int m = 0; m < Mw; m += 2) {
+    const int i = S * m + l - pad, ib = i + S;
+    const bool two = m + 1 < Mw;                           // wave-uniform
+    const bool la = valid && i >= 1 && i <= nct, lb = valid && two && ib >= 1 && ib <= nct;
+    uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+    if (la) Ca = ld16(rec + 16 * i);
+    if (lb) Cb = ld16(rec + 16 * ib);
+    const uint4 Ba = blk(i, la, Ca), Bb = blk(ib, lb, Cb);
+    const uint4 Ya = xor4(m == 0 ? Y : gf_mul8(Y, lds, gl), Ba);
+    if (m < M) Y = Ya;
+    if (two) {
+      const uint4 Yb = xor4(gf_mul8(Y, lds, gl), Bb);
+      if (m + 1 < M) Y = Yb;
+    }
+  }
+  uint4 tag = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
+  if (valid) {
+    ej0 = p.ej0[di];
+    if (DIR == 0) {
+      const uint32_t *q = reinterpret_cast<const uint32_t *>(rec + len - mlen);
+      if (mlen == 16) {
+        tag = ld16(rec + len - mlen);
+      } else {
+        tag.x = q[0];
+        tag.y = q[1];
+        if (mlen > 8) tag.z = q[2];
+      }
+    }
+  }
+  uint4 Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+#pragma unroll
+  for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
+  const uint4 T = xor4(Z, ej0);
+  int ok = 1;
+  if (valid) {
+    if (DIR == 1) {
+      if (l == 0) st_partial(rec + len - mlen, T, (int)mlen);
+    } else {
+      const uint4 d = mask_block(xor4(T, tag), (int)mlen);
+      ok = ((d.x | d.y | d.z | d.w) == 0);
+    }
+  }
+  if (have && l == 0) {
+    p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+    if (want_trl && !(valid && ok)) p.trailer[di] = 0;
+  }
+}
+
+// KIND 0: the ctr pass (S = kCtrLanes, T-table in LDS); KIND 1: the tag pass
+// (S lanes per record, the H^S GHASH table in LDS).  Chunks, tickets and the
+// non-AEAD chunk rule as gcm_kernel.
+template <int KIND, int DIR, int WG, int S>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GCM_SPLIT_WPE)))
+void gcm_split_kernel(GcmParams p) {
+  constexpr int RPW = 64 / S;
+  constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[65536];
+  const int tid = threadIdx.x;
+  if (KIND == 0) {
+    for (int idx = tid; idx < 256 * 32; idx += WG) {
+      const int x = idx >> 5, r = idx & 31;
+      const uint2 t = p.tpair[x];
+      *reinterpret_cast<uint32_t *>(lds + x * 256 + r * 4) = t.x;
+      *reinterpret_cast<uint32_t *>(lds + x * 256 + 128 + r * 4) = t.y;
+    }
+  }
+  const bool implicit = (p.chunks == nullptr);
+  const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
+  uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
+  const int wave = tid >> 6;
+  __shared__ uint32_t s_ticket[2];
+  for (uint32_t it = 0;; ++it) {
+    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
+    __syncthreads();
+    const uint32_t c = s_ticket[it & 1];
+    if (c >= nch) break;
+    uint32_t sa, start, count;
+    if (implicit) {
+      start = c * p.chunk;
+      count = min(p.chunk, p.n - start);
+      sa = p.desc[start].sa;
+    } else {
+      const Chunk ch = p.chunks[c];
+      sa = ch.sa;
+      start = ch.start;
+      count = ch.count;
+    }
+    sa = __builtin_amdgcn_readfirstlane(sa);
+    if (sa != cur_sa) {
+      __syncthreads();
+      if (sa < p.nsas) {
+        const DevSA *sp = p.sas + sa;
+        nr = sp->nr;
+        flags = sp->flags;
+        mlen = sp->mlen;
+        mode = sp->mode;
+        if (KIND == 1 && mode == ESPGPU_CSP_MODE_AEAD) {
+          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + gh8);
+          uint4 *dst = reinterpret_cast<uint4 *>(lds);
+#pragma unroll 4
+          for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+        }
+      } else {
+        mode = 0;
+      }
+      cur_sa = sa;
+      __syncthreads();
+    }
+    for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * RPW) {
+      const uint32_t rl = sub + (uint32_t)wave * RPW + (uint32_t)((tid & 63) / S);
+      const bool have = rl < count;
+      const uint32_t pos = start + (have ? rl : 0);
+      const uint32_t di = p.order ? p.order[pos] : pos;
+      if (mode != ESPGPU_CSP_MODE_AEAD) {
+        // the tag pass owns the statuses: EINVAL unless the ETA kernel's record
+        if (KIND == 1 && have && (tid & (S - 1)) == 0) {
+          const uint32_t rsa = p.desc[di].sa;
+          const bool eta = rsa < p.nsas && p.sas[rsa].mode == ESPGPU_CSP_MODE_ETA;
+          if (!eta) {
+            p.status[di] = ESPGPU_EINVAL;
+            if (DIR == 0 && p.trailer) p.trailer[di] = 0;
+          }
+        }
+        continue;
+      }
+      if (KIND == 0)
+        ctr_group<DIR>(p, lds, di, have, sa, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
+      else
+        tag_group<DIR, S>(p, lds, di, have, sa, flags, mlen);
+    }
+  }
+  if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
+    atomicExch(&p.queue[0], 0u);
+    atomicExch(&p.queue[1], 0u);
+  }
+}
+
 // S lanes per record: kGcmLanesPerRec for throughput, kGcmLanesSmall for
 // batches too small to fill the chip (half the serial steps per record).
 template <int MODE, int WG, int S>
@@ -715,6 +1016,24 @@ int set_gcm_opts(uint32_t opts) {
 #endif
 }
 
+// The split design for a large batch (ctr and tag passes, see gcm_split_kernel):
+// kernels on one stream, each resetting its ticket counters before the next starts.
+static int launch_gcm_split(const GcmParams &p, int encrypt, int two_pass, int grid, hipStream_t st) {
+  constexpr int WG = 1024, S = kGcmLanesPerRec;
+  if (encrypt) {
+    hipLaunchKernelGGL((gcm_split_kernel<0, 1, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 1, WG, S>), dim3(grid), dim3(WG), 0, st, p);
+  } else if (two_pass) {
+    hipLaunchKernelGGL((gcm_split_kernel<0, 3, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_split_kernel<0, 2, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
+  } else {
+    hipLaunchKernelGGL((gcm_split_kernel<0, 0, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
@@ -733,7 +1052,11 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
   const uint32_t rpw = 64 / (small ? W : kGcmLanesPerRec), per = (pp.n + (uint32_t)grid - 1) / (uint32_t)grid;
   p.chunk = 4 * rpw;
   while (p.chunk < per && p.chunk < (uint32_t)kChunkRecs) p.chunk <<= 1;
+#if GCM_WG != 1024
+  if (!small) p.chunk = (GCM_WG / 64) * (64 / kGcmLanesPerRec);   // experiment: one pass per chunk
+#endif
   if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + p.chunk - 1) / p.chunk)));
+  if (!small && p.ej0 != nullptr) return launch_gcm_split(p, encrypt, two_pass, grid, st);
   if (small) {
     if (encrypt)
       hipLaunchKernelGGL((gcm_kernel<1, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
@@ -742,11 +1065,11 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
     else
       hipLaunchKernelGGL((gcm_kernel<0, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
   } else if (encrypt) {
-    hipLaunchKernelGGL((gcm_kernel<1, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<1, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
   } else if (two_pass) {
-    hipLaunchKernelGGL((gcm_kernel<2, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<2, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
   } else {
-    hipLaunchKernelGGL((gcm_kernel<0, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<0, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -148,6 +148,12 @@ struct espgpu_ctx {
   // GCM lanes per record: 0 = by batch size, 4 or 8 forced (set_tuning
   // "gcm_lanes": the tests run both kernels at every batch size)
   int gcm_lanes = 0;
+  // GCM design for large batches (set_tuning "gcm_split"): 0 = the fused
+  // kernel, 1 = the ctr pass + tag pass (esp_gcm.hip gcm_split_kernel), which
+  // keep E_K(J0) per record in d_ej0
+  int gcm_split = 0;
+  uint4 *d_ej0 = nullptr;
+  uint32_t ej0_cap = 0;
   // planner workspace
   uint32_t plan_cap = 0;
   uint32_t *d_work = nullptr, *d_order = nullptr, *d_nchunks = nullptr;
@@ -367,6 +373,16 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
+  if ((kinds & 1) && c->gcm_split && (c->gcm_lanes == kGcmLanesPerRec || (c->gcm_lanes == 0 && n >= kGcmSmallBatch))) {
+    if (n > c->ej0_cap) {
+      hipFree(c->d_ej0);
+      c->d_ej0 = nullptr;
+      c->ej0_cap = 0;
+      HIPCHK(c, hipMalloc(&c->d_ej0, (size_t)n * sizeof(uint4)));
+      c->ej0_cap = n;
+    }
+    p.ej0 = c->d_ej0;
+  }
   if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, c->gcm_lanes, st))
     return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if ((kinds & 2) && c->n_eta > 0) {
@@ -492,6 +508,7 @@ void espgpu_fini(espgpu_ctx *c) {
   }
   hipFree(c->d_sas); hipFree(c->d_gtab); hipFree(c->d_tpair); hipFree(c->d_dpair); hipFree(c->d_isbox);
   hipFree(c->d_queue);
+  hipFree(c->d_ej0);
   hipFree(c->d_work); hipFree(c->d_order); hipFree(c->d_chunks); hipFree(c->d_nchunks);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -1227,6 +1244,11 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
     c->eta_fused = value;
     return 0;
   }
+  if (!strcmp(key, "gcm_split")) {
+    if (value != 0 && value != 1) return ESPGPU_EINVAL;
+    c->gcm_split = value;
+    return 0;
+  }
   if (!strcmp(key, "gcm_lanes")) {
     if (value != 0 && value != kGcmLanesPerRec && value != kGcmLanesSmall) return ESPGPU_EINVAL;
     c->gcm_lanes = value;
@@ -1235,6 +1257,12 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!strcmp(key, "overflow_mb")) {
     if (value < 0 || value > 65536) return ESPGPU_EINVAL;
     c->ovf_cap = (size_t)value << 20;
+    // reserved up front: growing the overflow inside process() would copy it
+    // (hundreds of microseconds at a few MiB)
+    const size_t rb = std::min(c->ovf_cap, (size_t)64 << 20), re = std::min(c->ovf_cap / 256, (size_t)1 << 18);
+    c->ovf.bytes.reserve(rb);
+    c->ovf.ent.reserve(re);
+    c->ovf.segpool.reserve(re);
     return 0;
   }
   if (!strcmp(key, "xfer")) {

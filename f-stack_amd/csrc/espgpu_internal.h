@@ -86,6 +86,7 @@ struct GcmParams {
   uint32_t *queue;
   uint32_t *trailer;              // decrypt: fused esp_input_cb trailer words, or nullptr
   uint32_t chunk;                 // implicit mode: records per chunk (launch_gcm sets it)
+  uint4 *ej0;                     // split design: E_K(J0) per descriptor (nullptr: fused kernel)
 };
 
 struct EtaParams {

@@ -326,6 +326,9 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *   "grid"      workgroups per launch (0 = 256, one per CU);
  *   "gcm_lanes" GCM lanes per record: 0 (default) 8 below 32768 records,
  *               else 4; 4 or 8 forces one kernel; others EINVAL;
+ *   "gcm_split" GCM batches of >= 32768 records (or any size with gcm_lanes
+ *               4): 1 = a CTR pass (16 lanes per record) then a GHASH / tag
+ *               pass, 0 = the fused kernel;
  *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
  *               decrypt (MODE 3) out of place, 1 one fused pass per record
  *               (MODE 0), 0 separate verify / decrypt kernels; others EINVAL;

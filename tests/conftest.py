@@ -35,13 +35,18 @@ def pytest_configure(config):
     _make(["-C", "f-stack_amd", "-j8"])
 
 
-@pytest.fixture(params=[4, 8], ids=["lanes4", "lanes8"])
+@pytest.fixture(params=[(4, 0), (8, 0), (4, 1)], ids=["lanes4", "lanes8", "split"])
 def gcm_lanes(request, drv):
-    """Run a GCM test through both kernels whatever its batch size: 4 lanes
-    per record (the throughput kernel) and 8 (the small-batch kernel, half
-    the serial steps); set_tuning "gcm_lanes", reset afterwards."""
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", request.param) == 0
+    """Run a GCM test through every GCM kernel design whatever its batch
+    size: the fused kernel with 4 lanes per record (throughput) and with 8
+    (small batches, half the serial steps), and the split design (a CTR pass
+    then a GHASH / tag pass); set_tuning "gcm_lanes" / "gcm_split", reset
+    afterwards."""
+    lanes, split = request.param
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", lanes) == 0
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", split) == 0
     try:
-        yield request.param
+        yield lanes
     finally:
         drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", 0)
+        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0)

@@ -271,7 +271,8 @@ def test_invalid_records_einval(drv):
     drv.freesession(sids[0])
 
 
-def test_full_size_1m_x_1500_vs_oracle(drv):
+@pytest.mark.parametrize("split", [0, 1], ids=["fused", "split"])
+def test_full_size_1m_x_1500_vs_oracle(drv, split):
     """cfg1 at full size (1M x 1500-B packets, one AES-128-GCM SA), every
     record against the oracle: GPU encrypt gives the oracle's arena byte for
     byte; with 1% of the ICVs flipped, GPU decrypt gives the oracle's 1M
@@ -289,6 +290,7 @@ def test_full_size_1m_x_1500_vs_oracle(drv):
     d["len"] = rec
     d["salt"] = int.from_bytes(sas[0].salt, "little")
     nth = min(16, os.cpu_count() or 1)
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", split) == 0
     ct = plain.copy()
     O.batch([sas[0].oracle], ct, d["off4"], d["len"], d["sa"], nthreads=nth, encrypt=True)
     d["sa"] = sids[0]
@@ -327,6 +329,7 @@ def test_full_size_1m_x_1500_vs_oracle(drv):
             assert np.array_equal(res[ok_mask], ref_out[ok_mask])
         del src, out, res
     drv.freesession(sids[0])
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0) == 0
 
 
 def test_freesession_waits_for_batch_on_user_stream(drv):
