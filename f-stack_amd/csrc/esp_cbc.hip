@@ -53,7 +53,16 @@ constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
 constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode == 6 ? 65536u : 163840u; }
 
+#ifndef ETA_HMAC_PREFETCH
+#define ETA_HMAC_PREFETCH 0
+#endif
+
 constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
+// MODE 2 / 3 session sets (the CKS template argument): every ETA session, or
+// split by hash so that the common kernel carries no SHA-512 code (its
+// registers then fit without spilling): HMAC-SHA1 / SHA2-256 / none, or
+// HMAC-SHA2-384 / 512 only
+constexpr int CK_ALL = -1, CK_NARROW = -2, CK_WIDEH = -3;
 constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
 
 typedef const __attribute__((address_space(4))) uint32_t *kptr;
@@ -429,16 +438,36 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
 #pragma unroll
   for (int k = 0; k < 8; ++k) h[k] = k < W ? ipad[k] : 0u;
   uint32_t w[16];
+#if ETA_HMAC_PREFETCH
+  // the next full block's 64 bytes are loaded while this one is compressed
+  uint4 nx[4];
+  if (nfull > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nx[q] = ld16(rec + 16 * q);
+  }
+#endif
   // One compression site for every block (inner data, inner padding, outer)
   // keeps a single inlined copy of the rounds.
   for (uint32_t b = 0; b <= total; ++b) {
     if (b < nfull) {
+#if ETA_HMAC_PREFETCH
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = bswap4(nx[q]);
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
+      if (b + 1 < nfull) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[q] = ld16(rec + 64 * (b + 1) + 16 * q);
+      }
+#else
       const uint8_t *p = rec + 64 * b;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint4 v = bswap4(ld16(p + 16 * q));
         w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
       }
+#endif
     } else if (b < total) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
@@ -872,6 +901,9 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         have = false;                                       // the fused launches' session
       } else if ((MODE == 5 || MODE == 6) && two_pass_only(s->calg, s->aalg)) {
         have = false;                                       // MODE 3's session
+      } else if ((MODE == 2 || MODE == 3) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
+                                              (CKS == CK_WIDEH && !wide_hash(s->aalg)))) {
+        have = false;                                       // the other hash set's launch
       } else {
         const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM, null = s->calg == ESPGPU_CRYPTO_NULL_CBC;
         const uint32_t mlen = s->mlen;
@@ -888,7 +920,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
-          if (MODE == 6) {              // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
+          if (MODE == 6 || CKS == CK_NARROW) {   // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
             if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
               hmac_t<HS_SHA256>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
                                 kp(s->opad), dg);
@@ -1146,14 +1178,17 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     // in place: the verify-first kernel (MODE 2); out of place: MODE 3 for
     // every session (eta_fused = 2, the default), or the one-pass MODE 0
     // kernel per cipher plus MODE 3 for SHA2-384/512 (eta_fused = 1)
+    // (kinds bit 4: HMAC-SHA2-384/512 sessions exist, served by their own launch)
     if (in_place) {
-      hipLaunchKernelGGL((eta_kernel<2, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else if (p.two_pass_all) {
-      hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      hipLaunchKernelGGL((eta_kernel<3, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else {
       if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     }
   } else {
     // verify pass (lane = record HMAC, status), then the block-parallel
@@ -1163,7 +1198,7 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
       hipLaunchKernelGGL((eta_kernel<6, 768, -1>), dim3(clamp(2 * grid, 768)), dim3(768), 0, st, p);
       hipLaunchKernelGGL((eta_kernel<5, 1024, -1>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
     }
-    if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -35,6 +35,7 @@ struct Session {
   int mode = 0, flags = 0, mlen = 0, klen = 0;
   bool ctr = false;       // ETA / CIPHER with AES-ICM (RFC 3686 ESP AES-CTR)
   bool null = false;      // ETA / CIPHER with CRYPTO_NULL_CBC (ESP-NULL)
+  bool whash = false;     // HMAC-SHA2-384/512 (128-byte hash blocks)
   bool wide = false;      // served by the two-pass ETA kernels only: HMAC-SHA2-384/512
                           // (128-byte hash blocks), no auth (CIPHER) or ESP-NULL
 };
@@ -138,6 +139,7 @@ struct espgpu_ctx {
   // ETA sessions: all, and by kernel: narrow-hash (SHA-1 / SHA2-256) CBC and
   // CTR, wide-hash (SHA2-384/512) CBC and CTR
   int n_eta = 0, n_cbc = 0, n_ctr = 0, n_wcbc = 0, n_wctr = 0;
+  int n_whash = 0;   // ETA sessions with HMAC-SHA2-384/512 (the wide-hash two-pass kernels)
   // ETA decrypt kernels (launch_eta; set_tuning "eta_fused"): 2 (default) =
   // out of place the verify-first two-pass kernel (MODE 3: HMAC lane = record,
   // then the block-parallel decrypt of the verified records into out; cfg3
@@ -403,7 +405,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.status = d_status;
     q.nsas = nsas;
     const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wcbc > 0 ? 4 : 0) |
-                   (c->n_wctr > 0 ? 8 : 0);
+                   (c->n_wctr > 0 ? 8 : 0) | (c->n_whash > 0 ? 16 : 0);
     q.two_pass_all = c->eta_fused == 2;
     if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, c->eta_fused != 0, st))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
@@ -657,11 +659,12 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   const bool eta_kind = csp->csp_mode != ESPGPU_CSP_MODE_AEAD;
   s.ctr = eta_kind && csp->csp_cipher_alg == ESPGPU_CRYPTO_AES_ICM;
   s.null = eta_kind && null_cipher;
-  s.wide = eta_kind && (sa.aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || sa.aalg == ESPGPU_CRYPTO_SHA2_512_HMAC ||
-                        sa.aalg == 0 || null_cipher);
+  s.whash = eta_kind && (sa.aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || sa.aalg == ESPGPU_CRYPTO_SHA2_512_HMAC);
+  s.wide = s.whash || (eta_kind && (sa.aalg == 0 || null_cipher));
   if (eta_kind) {
     c->n_eta++;
     eta_count(c, s)++;
+    c->n_whash += s.whash ? 1 : 0;
   }
   c->h_sas[slot] = sa;
   *sid_out = slot;
@@ -685,6 +688,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   if (fs.mode != ESPGPU_CSP_MODE_AEAD) {
     c->n_eta--;
     eta_count(c, fs)--;
+    c->n_whash -= fs.whash ? 1 : 0;
   }
   c->sessions[sid] = Session();
   DevSA z;
