@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "f-stack_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GUIDE_COPY_GBS = 6290.0        # the guide's measured float4 copy, 79 % of peak (MI355X_MICROARCH.md:36)
 CONFIGS = {
     "cfg0": dict(workload="cfg0: 64K x 64B ESP AES-128-GCM decrypt, single SA", packets=1 << 16,
                  pkt=64, skip=20, klen=16, nsa=1, mixed=False, alg="gcm"),
@@ -257,6 +258,9 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel_ms": round(kern_ms, 4)},
     }
+    # against the guide's measured copy ceiling (a torch copy here reaches less)
+    result["roofline"]["guide_copy_gbs"] = GUIDE_COPY_GBS
+    result["roofline"]["frac_of_guide_copy"] = round(achieved / GUIDE_COPY_GBS, 4)
     try:
         copy = hbm_copy_gbs(arena)
         result["roofline"]["hbm_copy_gbs"] = round(copy, 1)

@@ -53,6 +53,12 @@ constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
 constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode == 6 ? 65536u : 163840u; }
 
+#ifndef ETA_WG3
+#define ETA_WG3 768
+#endif
+#ifndef ETA_HMAC_PAIR
+#define ETA_HMAC_PAIR 0
+#endif
 #ifndef ETA_HMAC_PREFETCH
 #define ETA_HMAC_PREFETCH 0
 #endif
@@ -446,9 +452,30 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
     for (int q = 0; q < 4; ++q) nx[q] = ld16(rec + 16 * q);
   }
 #endif
+#if ETA_HMAC_PAIR
+  // full blocks two at a time: the 128 bytes are loaded together, so every
+  // cache line of the record is consumed within one step
+  uint32_t b = 0;
+  for (; b + 1 < nfull; b += 2) {
+    uint4 q8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) q8[q] = ld16(rec + 64 * b + 16 * q);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = bswap4(q8[4 * half + q]);
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
+      Hash<HS>::compress(h, w);
+    }
+  }
+  for (; b <= total; ++b) {
+#else
   // One compression site for every block (inner data, inner padding, outer)
   // keeps a single inlined copy of the rounds.
   for (uint32_t b = 0; b <= total; ++b) {
+#endif
     if (b < nfull) {
 #if ETA_HMAC_PREFETCH
 #pragma unroll
@@ -1183,7 +1210,7 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
       hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else if (p.two_pass_all) {
-      hipLaunchKernelGGL((eta_kernel<3, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else {
       if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);

@@ -68,26 +68,33 @@ __global__ __launch_bounds__(PWG) void plan_count(const espgpu_desc *desc, uint3
 }
 
 // Single workgroup.  gcnt[nkeys] -> gcur[nkeys] (record cursor), chunks.
+// Scan of the per-key record and chunk counts (each thread sums a run of
+// keys, Hillis-Steele over the 1024 partials), per-key offsets into LDS,
+// then every thread emits chunks c = tid, tid + 1024, ...: the key of chunk c
+// is the last key whose first chunk is <= c (binary search in LDS), so the
+// chunk list is written evenly by all threads whatever the key sizes.  (The
+// kernel takes ~33 us for 1K ETA sessions either way; the serial per-thread
+// emission it replaced was not its cost.)
 __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t nsas,
                                                  uint32_t *gcur, Chunk *chunks,
                                                  uint32_t *nchunks, uint32_t max_chunks) {
   __shared__ uint32_t s_rec[PWG], s_chk[PWG];
+  // per key: first chunk, first record (s_roff[nkeys] = all records)
+  __shared__ uint32_t s_coff[kMaxLdsKeys], s_roff[kMaxLdsKeys + 1];
   const uint32_t nkeys = num_keys(nsas);
   const uint32_t per = (nkeys + PWG - 1) / PWG;
   const uint32_t k0 = threadIdx.x * per, k1 = min(nkeys, k0 + per);
   const uint32_t eta0 = 4 * nsas + 1;                       // first ETA key
   auto recs_per_chunk = [&](uint32_t k) { return k >= eta0 ? 64u : (uint32_t)kChunkRecs; };
-  uint32_t r = 0, c = 0, cg = 0;
+  uint32_t r = 0, c = 0;
   for (uint32_t k = k0; k < k1; ++k) {
-    r += gcnt[k];
-    const uint32_t nc = (gcnt[k] + recs_per_chunk(k) - 1) / recs_per_chunk(k);
-    c += nc;
-    if (k < eta0) cg += nc;
+    const uint32_t cnt = gcnt[k];
+    r += cnt;
+    c += (cnt + recs_per_chunk(k) - 1) / recs_per_chunk(k);
   }
   s_rec[threadIdx.x] = r;
   s_chk[threadIdx.x] = c;
   __syncthreads();
-  // Hillis-Steele inclusive scan over 1024 partials
   for (int o = 1; o < PWG; o <<= 1) {
     uint32_t a = threadIdx.x >= (unsigned)o ? s_rec[threadIdx.x - o] : 0;
     uint32_t b = threadIdx.x >= (unsigned)o ? s_chk[threadIdx.x - o] : 0;
@@ -97,28 +104,40 @@ __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t 
     __syncthreads();
   }
   uint32_t roff = s_rec[threadIdx.x] - r, coff = s_chk[threadIdx.x] - c;
-  // the thread holding key eta0 (or the first one past the GCM keys) knows
-  // where the ETA chunks begin
-  if (k0 <= eta0 && eta0 < k1) nchunks[0] = min(coff + cg, max_chunks);
   for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t cnt = gcnt[k], rpc = recs_per_chunk(k);
-    gcur[k] = roff;
+    const uint32_t cnt = gcnt[k];
+    gcur[k] = roff;                       // record cursor (plan_scatter) = the key's first record
+    s_roff[k] = roff;
+    s_coff[k] = coff;
+    roff += cnt;
+    coff += (cnt + recs_per_chunk(k) - 1) / recs_per_chunk(k);
+  }
+  if (threadIdx.x == PWG - 1) s_roff[nkeys] = s_rec[PWG - 1];
+  __syncthreads();
+  const uint32_t total = s_chk[PWG - 1];
+  if (threadIdx.x == 0) {
+    nchunks[1] = min(total, max_chunks);
+    // the GCM kernel's share: the chunks before the first ETA key
+    nchunks[0] = eta0 < nkeys ? min(s_coff[eta0], max_chunks) : nchunks[1];
+  }
+  const uint32_t lim = min(total, max_chunks);
+  for (uint32_t ci = threadIdx.x; ci < lim; ci += PWG) {
+    uint32_t lo = 0, hi = nkeys;                          // last key with s_coff <= ci
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_coff[mid] <= ci) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t k = lo, cnt = s_roff[k + 1] - s_roff[k], rpc = recs_per_chunk(k);
     const uint32_t sa = k == 4 * nsas ? 0xffffffffu : (k >= eta0 ? k - eta0 : k % nsas);
     const uint32_t cls = k >= 4 * nsas ? 4u : 3u - k / nsas;
     // ceil(cnt / rpc) chunks of EQUAL size (270 records -> 135 + 135, not
     // 256 + 14): a workgroup's pass time grows with its busy waves, so a
     // near-empty remainder chunk costs almost a full pass (cfg2: 1K sessions
     // x 4 size classes leave ~256 +- 16 records per key)
-    const uint32_t nc = (cnt + rpc - 1) / rpc;
-    for (uint32_t j = 0; j < nc; ++j, ++coff) {
-      const uint32_t a = (uint32_t)((uint64_t)cnt * j / nc), b = (uint32_t)((uint64_t)cnt * (j + 1) / nc);
-      if (coff < max_chunks) chunks[coff] = Chunk{sa, roff + a, b - a, cls};
-    }
-    roff += cnt;
-  }
-  if (threadIdx.x == PWG - 1) {
-    nchunks[1] = min(s_chk[PWG - 1], max_chunks);
-    if (eta0 >= nkeys) nchunks[0] = nchunks[1];             // no sessions: no ETA keys
+    const uint32_t nc = (cnt + rpc - 1) / rpc, jj = ci - s_coff[k];
+    const uint32_t a = (uint32_t)((uint64_t)cnt * jj / nc), b = (uint32_t)((uint64_t)cnt * (jj + 1) / nc);
+    chunks[ci] = Chunk{sa, s_roff[k] + a, b - a, cls};
   }
 }
 

@@ -111,6 +111,11 @@ def test_probesession_accepts_esp_cbc_sha1():
          csp_auth_alg=7, csp_auth_klen=20),                                                 # ESP-NULL with a key
     dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=25, csp_cipher_klen=16,
          csp_auth_mlen=4),                                                                  # GCM ICV 4 (not RFC 4106)
+    # ESP AES-GMAC (SADB_X_EALG_AESGMAC, key.c:591, RFC 4543): esp_init makes
+    # it CSP_MODE_CIPHER with CRYPTO_AES_NIST_GMAC (xform_esp.c:230-236), which
+    # check_csp refuses (alg_is_cipher: GMAC is ALG_KEYED_DIGEST, crypto.c:682,
+    # :747-783), so crypto_newsession fails on the reference too
+    dict(csp_mode=2, csp_ivlen=12, csp_cipher_alg=24, csp_cipher_klen=16),
     dict(csp_mode=L.CSP_MODE_AEAD, csp_flags=0x1, csp_ivlen=12, csp_cipher_alg=25,
          csp_cipher_klen=16),                                                               # SEPARATE_OUTPUT
     dict(csp_mode=L.CSP_MODE_AEAD, csp_ivlen=12, csp_cipher_alg=25, csp_cipher_klen=16,

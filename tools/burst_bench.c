@@ -177,6 +177,19 @@ int main(int argc, char **argv)
 	memset(&cfg, 0, sizeof(cfg));
 	CK(espgpu_init(&cfg, &ctx));
 	calibrate_tsc();
+	/* BURST_TUNING="key=v,key=v": set_tuning before the runs (measurement knobs) */
+	const char *tun = getenv("BURST_TUNING");
+	if (tun) {
+		char buf[256];
+		snprintf(buf, sizeof buf, "%s", tun);
+		for (char *kv = strtok(buf, ","); kv; kv = strtok(NULL, ",")) {
+			char *eq = strchr(kv, '=');
+			if (!eq) continue;
+			*eq = 0;
+			CK(espgpu_set_tuning(ctx, kv, atoi(eq + 1)));
+		}
+	}
+	const int only_mode = getenv("BURST_MODE") ? atoi(getenv("BURST_MODE")) : -1;
 	uint8_t key[16], salt[4] = {1, 2, 3, 4};
 	for (int i = 0; i < 16; i++) key[i] = (uint8_t)(i * 13 + 5);
 	struct espgpu_session_params p;
@@ -211,8 +224,13 @@ int main(int argc, char **argv)
 		make_req(&req[i], &seg[i], rec_of(i), sid, 0, salt);
 	}
 
+	int registered = 0;
 	for (int mode = 0; mode < 2; mode++) {
-		if (mode == 1) CK(espgpu_register_host(ctx, bufs, bytes));
+		if (only_mode >= 0 && mode != only_mode) continue;
+		if (mode == 1) {
+			CK(espgpu_register_host(ctx, bufs, bytes));
+			registered = 1;
+		}
 		for (int xfer = 1; xfer >= 0; xfer--) {
 			CK(espgpu_set_tuning(ctx, "xfer", xfer));
 			for (int bi = 0; bi < nb; bi++) {
@@ -261,7 +279,7 @@ int main(int argc, char **argv)
 			}
 		}
 	}
-	CK(espgpu_unregister_host(ctx, bufs));
+	if (registered) CK(espgpu_unregister_host(ctx, bufs));
 	espgpu_freesession(ctx, sid);
 	espgpu_fini(ctx);
 	return 0;
