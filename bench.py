@@ -297,11 +297,12 @@ def launched_kernel(cfg, inplace):
     prices): gcm_kernel<MODE, 1024, S> with MODE 0 = out-of-place decrypt, 2 =
     in-place verify-first, S = 4 lanes per record (every bench config has
     >= 32K records: the small-batch S = 8 kernel is not launched);
-    eta_kernel<3 (out of place) / 2 (in place), 768, -1> for CBC + HMAC-SHA1
-    (verify pass, then the block-parallel decrypt of the verified records)."""
+    eta_kernel<3 (out of place) / 2 (in place), 768, -2> for CBC + HMAC-SHA1
+    (verify pass, then the block-parallel decrypt of the verified records; -2 =
+    the launch for SHA-1 / SHA2-256 sessions, esp_cbc.hip CK_NARROW)."""
     if cfg["alg"] == "gcm":
         return "gcm_kernel<%d, 1024, 4>" % (2 if inplace else 0)
-    return "eta_kernel<2, 768, -1>" if inplace else "eta_kernel<3, 768, -1>"   # verify-first two-pass
+    return "eta_kernel<2, 768, -2>" if inplace else "eta_kernel<3, 768, -2>"   # verify-first two-pass
 
 
 def profile_traffic(config, inplace, kernel, kern_ms):

@@ -11,14 +11,15 @@ prof() {   # <name> <cfg> [--inplace]
   python tools/prof_summary.py gpurun_out/prof_${TAG}_$1 ${TAG}_$1 $2 $3 > gpurun_out/sum_${TAG}_$1.log 2>&1
   echo "profile $1 done"
 }
-prof cfg1 cfg1
-prof cfg2 cfg2
-prof cfg3 cfg3
-prof cfg4 cfg4
-prof cfg0 cfg0
-prof cfg1_inplace cfg1 --inplace
-cp profiles/${TAG}_*.json profiles/pmc_*.json gpurun_out/profiles/
-for c in cfg1 cfg0 cfg2 cfg3 cfg4; do
+# PROFS / BENCHES select a subset (a call has at most 20 minutes)
+for p in ${PROFS-cfg1 cfg2 cfg3 cfg4 cfg0 cfg1_inplace}; do
+  case $p in
+    cfg1_inplace) prof cfg1_inplace cfg1 --inplace ;;
+    *) prof $p $p ;;
+  esac
+done
+cp profiles/${TAG}_*.json profiles/pmc_*.json gpurun_out/profiles/ 2>/dev/null || true
+for c in ${BENCHES-cfg1 cfg0 cfg2 cfg3 cfg4}; do
   timeout -k 10 300 python bench.py --config $c > gpurun_out/bench_${TAG}_$c.json 2> gpurun_out/bench_${TAG}_$c.err
   echo "bench $c done"
 done
