@@ -27,6 +27,9 @@ using namespace espgpu;
 
 namespace {
 
+#ifndef GPU_TIME_SMALL
+#define GPU_TIME_SMALL 0
+#endif
 // flush(): batches up to this many staged bytes run on one stream (latency)
 constexpr uint32_t kSmallBatchBytes = 128u << 10;
 
@@ -111,6 +114,7 @@ struct Slot {
   std::vector<Pending> reqs;             // reserved to batch_records: no per-record allocation
   std::vector<espgpu_seg> segpool;       // segment lists of the staged requests
   hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, kout = nullptr, done = nullptr;
+  bool timed = false;                       // k0 / k1 recorded around the kernels
   hipStream_t st = nullptr;                 // small batches: copy, kernel, copy in order here
 };
 
@@ -935,14 +939,17 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
     }
   }
   if (nin && launch_xfer(s.h_xfer_dev, nin, nullptr, s_k)) return fail(c, ESPGPU_EIO, "xfer kernel launch failed");
-  hipEventRecord(s.k0, s_k);
+  // kernel timing events (stats.kernel_ns, espgpu_last_kernel_ms) only on
+  // large batches: on a burst's own stream each marker adds to its latency
+  s.timed = !small || GPU_TIME_SMALL;
+  if (s.timed) hipEventRecord(s.k0, s_k);
   // a single-session batch skips the device planner (ESPGPU_BATCH_GROUPED:
   // one session trivially satisfies "one session per chunk")
   int e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
                     dres + s.stat_off, s.op ? nullptr : s.d_out, s.mixed ? 0u : (uint32_t)ESPGPU_BATCH_GROUPED,
                     s.op, s_k, nullptr, s.kinds);
   if (e) return e;
-  hipEventRecord(s.k1, s_k);
+  if (s.timed) hipEventRecord(s.k1, s_k);
   if (nout && launch_xfer(s.h_xfer_dev + nin, nout, d_stat, s_k)) return fail(c, ESPGPU_EIO, "xfer kernel launch failed");
   if (!kcopy) {
     if (!small) {
@@ -985,7 +992,7 @@ int espgpu_flush(espgpu_ctx *c) {
 
 static int complete_slot(espgpu_ctx *c, Slot &s) {
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) {
+  if (s.timed && hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) {
     c->last_ms = ms;
     c->stats.kernel_ns += (uint64_t)(ms * 1e6);
   }

@@ -318,8 +318,10 @@ int  espgpu_replay_merge(espgpu_ctx *ctx, uint8_t *d_status, const uint8_t *d_rs
  * in arrival order per SA: 0 (window advanced / bit set) or ESPGPU_EACCES. */
 int  espgpu_replay_update(struct espgpu_replay *r, uint32_t *bitmap, uint32_t seq);
 
-/* Device time of the last batch's crypto kernel (ms, from HIP events on the
- * batch stream), for the roofline accounting in bench.py. */
+/* Device time of the last timed batch's crypto kernels (ms, from HIP events
+ * on the batch stream).  Process-path batches of <= 128 KiB (a burst on its
+ * slot's own stream) are not timed: the two event markers cost a 32-record
+ * burst 8 us of its 65. */
 float espgpu_last_kernel_ms(espgpu_ctx *ctx);
 
 /* Tuning knobs (engine-internal, for A/B measurement):
