@@ -45,8 +45,15 @@
 #include <algorithm>
 
 #include "espgpu_internal.h"
+#include "xfer_copy.h"
 
 // Experiment switches (tools/variant.sh builds; defaults are the product)
+#ifndef GCM_SMALL_CHUNK_WAVES
+#define GCM_SMALL_CHUNK_WAVES 1
+#endif
+#ifndef GCM_PREFETCH
+#define GCM_PREFETCH 0
+#endif
 #ifndef GCM_STORE_LATE
 #define GCM_STORE_LATE 0
 #endif
@@ -149,6 +156,11 @@ __device__ __forceinline__ uint32_t te1(const uint8_t *lds, uint32_t a) {
 }
 
 // One middle round on big-endian state words; k = ror16(round key) (kernel form).
+// W (lone-wave kernels): a scheduling barrier between the 16 lookups and the
+// XORs, so every lookup is issued before the wave waits on the first; the
+// throughput kernels leave the interleaving (fewer live registers) to the
+// compiler and hide the latency with other waves.
+template <bool W = false>
 __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint4 k,
                                           const uint8_t *lds, uint32_t slot) {
   // column c: Te0[s_c.b3] ^ Te1[s_c+1.b2] ^ ror16(Te0[s_c+2.b1] ^ Te1[s_c+3.b0] ^ ror16(rk))
@@ -160,6 +172,7 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
   const uint32_t c2 = te0(lds, tpa(s0, slot, 1)), d2 = te1(lds, tpa(s1, slot, 0));
   const uint32_t a3 = te0(lds, tpa(s3, slot, 3)), b3 = te1(lds, tpa(s0, slot, 2));
   const uint32_t c3 = te0(lds, tpa(s1, slot, 1)), d3 = te1(lds, tpa(s2, slot, 0));
+  if (W) __builtin_amdgcn_sched_barrier(0);
   s0 = xor3(a0, b0, ror16(xor3(c0, d0, k.x)));
   s1 = xor3(a1, b1, ror16(xor3(c1, d1, k.y)));
   s2 = xor3(a2, b2, ror16(xor3(c2, d2, k.z)));
@@ -177,29 +190,48 @@ __device__ uint32_t g_opts;
 __device__ __forceinline__ uint32_t gopts() {
   return *(const __attribute__((address_space(4))) uint32_t *)(const void *)&g_opts;
 }
+// Phase clock of the small-batch kernel (knobs build only): workgroup 0's
+// thread 0 records (shader clock, 100 MHz real-time clock) at each phase
+// boundary of its first chunk; read with espgpu_debug_phases().
+__device__ uint64_t g_phase[32];
+#define GCM_PHASE_T(i, first, thr)                                          \
+  do {                                                                     \
+    if (S == kGcmLanesSmall && blockIdx.x == 0 && threadIdx.x == (thr) && (first)) { \
+      g_phase[2 * (i)] = __builtin_readcyclecounter();                     \
+      g_phase[2 * (i) + 1] = __builtin_amdgcn_s_memrealtime();             \
+    }                                                                      \
+  } while (0)
+#define GCM_PHASE(i, first) GCM_PHASE_T(i, first, 0)
 #else
 __device__ __forceinline__ constexpr uint32_t gopts() { return 0; }
+#define GCM_PHASE(i, first) do {} while (0)
+#define GCM_PHASE_T(i, first, thr) do {} while (0)
 #endif
 
 // Last round: S[x] is byte 1 of Te0[x]; emit little-endian (memory order)
 // words directly; the last round key is stored byte-swapped.
+template <bool W = false>
 __device__ __forceinline__ uint4 aes_last(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint4 k,
                                           const uint8_t *lds, uint32_t slot) {
-  uint32_t o[4];
+  uint32_t o[4], a[4], b[4], c[4], d[4];
   const uint32_t ss[4] = {s0, s1, s2, s3};
   const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
 #pragma unroll
   for (int col = 0; col < 4; ++col) {
-    const uint32_t a = te0(lds, tpa(ss[col], slot, 3));
-    const uint32_t b = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
-    const uint32_t c = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
-    const uint32_t d = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
-    o[col] = xor3(perm(b, a, 0x0c0c0501u), perm(d, c, 0x05010c0cu), kk[col]);
+    a[col] = te0(lds, tpa(ss[col], slot, 3));
+    b[col] = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
+    c[col] = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
+    d[col] = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
   }
+  if (W) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int col = 0; col < 4; ++col)
+    o[col] = xor3(perm(b[col], a[col], 0x0c0c0501u), perm(d[col], c[col], 0x05010c0cu), kk[col]);
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // Rounds r0..nr-1 (middle) and the last round.  s* = state entering round r0.
+template <bool W = false>
 __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, int r0,
                                             int nr, rkptr rk, const uint8_t *lds,
                                             uint32_t slot) {
@@ -208,10 +240,10 @@ __device__ __forceinline__ uint4 aes_rounds(uint32_t s0, uint32_t s1, uint32_t s
   // not LDS, which is the bottleneck resource.
 #pragma unroll 1
   for (int r = r0; r < nr; ++r) {
-    aes_round(s0, s1, s2, s3, ldk4(rk + 4 * r), lds, slot);
+    aes_round<W>(s0, s1, s2, s3, ldk4(rk + 4 * r), lds, slot);
     __builtin_amdgcn_sched_barrier(0);
   }
-  return aes_last(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
+  return aes_last<W>(s0, s1, s2, s3, ldk4(rk + 4 * nr), lds, slot);
 }
 
 // ---- counter-mode caching of rounds 1-2 ------------------------------------
@@ -255,6 +287,7 @@ __device__ __forceinline__ void ctr_cache_build(CtrCache &cc, uint32_t s0, uint3
 }
 
 // E_K(nonce || ctr) using the cache (which must be built for ctr >> 8).
+template <bool W = false>
 __device__ __forceinline__ uint4 aes_ctr(const CtrCache &cc, uint32_t ctr, uint32_t rk3, int nr,
                                          rkptr rk, const uint8_t *lds, uint32_t slot) {
   const uint32_t t0 = cc.K0 ^ ror16(te1(lds, tpa(ctr ^ rk3, slot, 0)));
@@ -262,12 +295,70 @@ __device__ __forceinline__ uint4 aes_ctr(const CtrCache &cc, uint32_t ctr, uint3
   const uint32_t v1 = cc.L1 ^ ror16(te1(lds, tpa(t0, slot, 0)));
   const uint32_t v2 = cc.L2 ^ ror16(te0(lds, tpa(t0, slot, 1)));
   const uint32_t v3 = cc.L3 ^ te1(lds, tpa(t0, slot, 2));
-  return aes_rounds(v0, v1, v2, v3, 3, nr, rk, lds, slot);
+  return aes_rounds<W>(v0, v1, v2, v3, 3, nr, rk, lds, slot);
+}
+
+// Two blocks' round with all 32 lookups issued before the XORs (lone wave).
+__device__ __forceinline__ void aes_round2w(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, uint32_t &u0,
+                                            uint32_t &u1, uint32_t &u2, uint32_t &u3, uint4 k,
+                                            const uint8_t *lds, uint32_t slot) {
+  const uint32_t ss[4] = {s0, s1, s2, s3}, uu[4] = {u0, u1, u2, u3};
+  uint32_t a[4], b[4], c[4], d[4], e[4], f[4], g[4], h[4];
+#pragma unroll
+  for (int col = 0; col < 4; ++col) {
+    a[col] = te0(lds, tpa(ss[col], slot, 3));
+    b[col] = te1(lds, tpa(ss[(col + 1) & 3], slot, 2));
+    c[col] = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
+    d[col] = te1(lds, tpa(ss[(col + 3) & 3], slot, 0));
+    e[col] = te0(lds, tpa(uu[col], slot, 3));
+    f[col] = te1(lds, tpa(uu[(col + 1) & 3], slot, 2));
+    g[col] = te0(lds, tpa(uu[(col + 2) & 3], slot, 1));
+    h[col] = te1(lds, tpa(uu[(col + 3) & 3], slot, 0));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+  uint32_t o[4], q[4];
+#pragma unroll
+  for (int col = 0; col < 4; ++col) {
+    o[col] = xor3(a[col], b[col], ror16(xor3(c[col], d[col], kk[col])));
+    q[col] = xor3(e[col], f[col], ror16(xor3(g[col], h[col], kk[col])));
+  }
+  s0 = o[0], s1 = o[1], s2 = o[2], s3 = o[3];
+  u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3];
+}
+
+__device__ __forceinline__ void aes_last2w(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t u0,
+                                           uint32_t u1, uint32_t u2, uint32_t u3, uint4 k, const uint8_t *lds,
+                                           uint32_t slot, uint4 &ka, uint4 &kb) {
+  const uint32_t ss[4] = {s0, s1, s2, s3}, uu[4] = {u0, u1, u2, u3};
+  const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+  uint32_t a[4], b[4], c[4], d[4], e[4], f[4], g[4], h[4];
+#pragma unroll
+  for (int col = 0; col < 4; ++col) {
+    a[col] = te0(lds, tpa(ss[col], slot, 3));
+    b[col] = te0(lds, tpa(ss[(col + 1) & 3], slot, 2));
+    c[col] = te0(lds, tpa(ss[(col + 2) & 3], slot, 1));
+    d[col] = te0(lds, tpa(ss[(col + 3) & 3], slot, 0));
+    e[col] = te0(lds, tpa(uu[col], slot, 3));
+    f[col] = te0(lds, tpa(uu[(col + 1) & 3], slot, 2));
+    g[col] = te0(lds, tpa(uu[(col + 2) & 3], slot, 1));
+    h[col] = te0(lds, tpa(uu[(col + 3) & 3], slot, 0));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t o[4], q[4];
+#pragma unroll
+  for (int col = 0; col < 4; ++col) {
+    o[col] = xor3(perm(b[col], a[col], 0x0c0c0501u), perm(d[col], c[col], 0x05010c0cu), kk[col]);
+    q[col] = xor3(perm(f[col], e[col], 0x0c0c0501u), perm(h[col], g[col], 0x05010c0cu), kk[col]);
+  }
+  ka = make_uint4(o[0], o[1], o[2], o[3]);
+  kb = make_uint4(q[0], q[1], q[2], q[3]);
 }
 
 // Two counter blocks (both covered by the cache) interleaved round by round:
 // each round issues 32 independent LDS lookups before the wave waits, halving
 // the dependent LDS round trips per block.
+template <bool W = false>
 __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32_t cb, uint32_t rk3,
                                          int nr, rkptr rk, const uint8_t *lds, uint32_t slot, uint4 &ka,
                                          uint4 &kb) {
@@ -281,13 +372,21 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32
 #pragma unroll 1
   for (int r = 3; r < ((gopts() & 4) ? 3 : nr); ++r) {
     const uint4 k = ldk4(rk + 4 * r);
-    aes_round(a0, a1, a2, a3, k, lds, slot);
-    aes_round(b0, b1, b2, b3, k, lds, slot);
+    if (W) {
+      aes_round2w(a0, a1, a2, a3, b0, b1, b2, b3, k, lds, slot);
+    } else {
+      aes_round(a0, a1, a2, a3, k, lds, slot);
+      aes_round(b0, b1, b2, b3, k, lds, slot);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   const uint4 kl = ldk4(rk + 4 * nr);
-  ka = aes_last(a0, a1, a2, a3, kl, lds, slot);
-  kb = aes_last(b0, b1, b2, b3, kl, lds, slot);
+  if (W) {
+    aes_last2w(a0, a1, a2, a3, b0, b1, b2, b3, kl, lds, slot, ka, kb);
+  } else {
+    ka = aes_last(a0, a1, a2, a3, kl, lds, slot);
+    kb = aes_last(b0, b1, b2, b3, kl, lds, slot);
+  }
 }
 
 // ---- GHASH multiply by a fixed power (gf_mul, gfmult.c:219-229) ----------
@@ -349,16 +448,51 @@ __device__ __forceinline__ uint4 gf_mul8(uint4 x, const uint8_t *lds, const GhLa
   return make_uint4(r0, r1, r2, r3);
 }
 
+// gf_mul8 for a lone wave (burst kernel, 256 VGPRs): all 16 lookups are
+// issued before any XOR (a scheduling barrier keeps them together), so the
+// multiply waits one LDS latency instead of the eight the register-lean form
+// above serializes (each pair's XOR frees its registers for the next pair).
+__device__ __forceinline__ uint4 gf_mul8_wide(uint4 x, const uint8_t *lds, const GhLane &g) {
+  const uint32_t a0 = g.sw1 ? x.y : x.x, a1 = g.sw1 ? x.x : x.y;
+  const uint32_t a2 = g.sw1 ? x.w : x.z, a3 = g.sw1 ? x.z : x.w;
+  const uint32_t w[4] = {g.sw2 ? a2 : a0, g.sw2 ? a3 : a1, g.sw2 ? a0 : a2, g.sw2 ? a1 : a3};
+  uint4 e[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t c = perm(w[k], w[k], g.selb);
+    const uint32_t cp = g.cpos0 ^ ((uint32_t)k * 0x40404040u);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t ea = perm(c, cp, 0x0c0c0000u | ((4u + b) << 8) | (uint32_t)b);
+      e[4 * k + b] = *reinterpret_cast<const uint4 *>(lds + LDS_GT + ea);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+  for (int q = 0; q < 16; q += 2) {
+    r0 = xor3(r0, e[q].x, e[q + 1].x);
+    r1 = xor3(r1, e[q].y, e[q + 1].y);
+    r2 = xor3(r2, e[q].z, e[q + 1].z);
+    r3 = xor3(r3, e[q].w, e[q + 1].w);
+  }
+  return make_uint4(r0, r1, r2, r3);
+}
+
 // Y * H^e with the 4-bit table of that power in global memory (t = its 8 KiB:
 // nibble position j (byte j>>1, low nibble if j even), value n at j*256+n*16).
 // Used once per record per lane (the final x H^(8-l)), where the power differs
 // per lane: from LDS that would be bank conflicts, from L2 it is a gather.
+// ROLLED: rolled over the 4 words (8 positions, 2 KiB of table each), so the
+// table addresses stay one pointer instead of 16 hoisted 64-bit ones (the
+// throughput kernels); unrolled, all 32 gathers are in flight at once instead
+// of four dependent L2 round trips (the small-batch kernels' latency).
+template <bool ROLLED = true>
 __device__ __forceinline__ uint4 gf_mul4_global(uint4 x, const uint8_t *t) {
   uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
   uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
-  // rolled over the 4 words (8 positions, 2 KiB of table each): the table
-  // addresses stay one pointer instead of 16 hoisted 64-bit ones
-#pragma unroll 1
+  constexpr int kUnroll = ROLLED ? 1 : 4;
+#pragma unroll kUnroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t hi = w & 0xF0F0F0F0u, lo = (w << 4) & 0xF0F0F0F0u;
 #pragma unroll
@@ -431,6 +565,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   int Mw = M;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) Mw = max(Mw, __shfl_xor(Mw, o));
+  GCM_PHASE(8, true);
   const bool want_trl = MODE != 1 && p.trailer != nullptr;
   if (Mw == 0) {
     if (have && l == 0 && !valid) p.status[di] = ESPGPU_EINVAL;
@@ -473,6 +608,13 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   };
 
   uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
+  // Experiment (GCM_PREFETCH, off): the small-batch kernel issuing each
+  // interior pair's ciphertext load one pair ahead.  Measured equal on a
+  // 32-record burst (the lone wave is VALU-issue-bound, not load-bound) and
+  // it makes the S = 8 kernels spill.
+  constexpr bool PF = GCM_PREFETCH && S == kGcmLanesSmall;
+  uint4 pCa = make_uint4(0, 0, 0, 0), pCb = make_uint4(0, 0, 0, 0);
+  int pf_m = -1;                                            // step held in pCa / pCb
   int m = 0;
   while (m < Mw) {
     const int i = S * m + l - pad;
@@ -491,9 +633,22 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         // unmasked.  Most pairs of a record take this path.
         if (__all(!valid || (i >= 1 && 16 * ib < ct_len))) {
           uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
-          if (valid && !(gopts() & 17)) {
+          if (PF && pf_m == m) {
+            Ca = pCa;
+            Cb = pCb;
+          } else if (valid && !(gopts() & 17)) {
             Ca = ld16(rec + 16 * i);
             Cb = ld16(rec + 16 * ib);
+          }
+          if (PF) {
+            // the next pair, if it is interior for this lane (in bounds): the
+            // next step takes the interior path only if it is for every lane
+            const int in = i + 2 * S, inb = in + S;
+            if (valid && 16 * inb < ct_len && !(gopts() & 17)) {
+              pCa = ld16(rec + 16 * in);
+              pCb = ld16(rec + 16 * inb);
+            }
+            pf_m = m + 2;
           }
           uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
           if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
@@ -573,6 +728,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     Y = xor4(Y, B);
     ++m;
   }
+  GCM_PHASE(9, true);
   // the received ICV, loaded before the final multiply's L2 gathers so the
   // two latencies overlap
   uint4 tag = make_uint4(0, 0, 0, 0);
@@ -588,11 +744,12 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
   uint4 Z = (gopts() & 64) ? Y
-                           : gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+                           : gf_mul4_global<true>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 ej0 = shfl4(EJ0, (lane & ~(S - 1)) | pad);
   const uint4 T = xor4(Z, ej0);
+  GCM_PHASE(10, true);
 
   int ok = 1;
   if (valid) {
@@ -649,14 +806,18 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
 // (writes the ICV); decrypt in place, verify first: ctr (DIR 3: E_K(J0)
 // only), tag, then ctr (DIR 2: only records whose status is 0).
 constexpr int kCtrLanes = 16;
+// Burst kernel (gcm_burst_kernel below): 512-thread workgroups, because two
+// waves per SIMD leave 256 VGPRs per lane (at 1024 threads the 128-VGPR cap
+// spilled 20-28) and a burst never needs the occupancy; its ctr pass runs 32
+// lanes per record on waves [0, kBurstCtrWaves), its hash pass the rest.
+constexpr int kBurstWG = 512, kBurstCtrLanes = 32, kBurstCtrWaves = 5;
 
-template <int DIR>
+template <int DIR, int S = kCtrLanes, bool W = false>
 __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
-                                          uint32_t sa, uint32_t mlen, int nr, rkptr rk) {
-  constexpr int S = kCtrLanes;
+                                          uint32_t sa, uint32_t mlen, int nr, rkptr rk, uint32_t tbase = 0) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
-  const uint32_t slot = (uint32_t)(lane & 31) * 4;        // T-table at LDS offset 0
+  const uint32_t slot = (uint32_t)(lane & 31) * 4 | tbase;  // T-table at LDS offset tbase (64 KiB aligned)
   int valid = 0, ct_len = 0, nct = 0, K = 0;
   uint8_t *rec = p.arena;
   uint32_t s0c = 0, s1c = 0, s2c = 0;
@@ -712,12 +873,12 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
     if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
     uint4 ka, kb = make_uint4(0, 0, 0, 0);
     if (!GCM_CTR_SINGLE && two && __all((int)(cb >> 8) == cc.hi)) {
-      aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+      aes_ctr2<W>(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
     } else {
-      ka = aes_ctr(cc, ca, rk3, nr, rk, lds, slot);
+      ka = aes_ctr<W>(cc, ca, rk3, nr, rk, lds, slot);
       if (two) {
         if ((int)(cb >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(cb >> 8), rk, lds, slot);
-        kb = aes_ctr(cc, cb, rk3, nr, rk, lds, slot);
+        kb = aes_ctr<W>(cc, cb, rk3, nr, rk, lds, slot);
       }
     }
     emit(ia, la, Ca, ka);
@@ -725,9 +886,13 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
   }
 }
 
+// zs != nullptr (burst kernel, decrypt): only the GHASH value, Z = sum of the
+// lanes' Y x H^(S-1-l), goes to zs[zi] (LDS); tag_finish completes the record
+// once E_K(J0) exists.
 template <int DIR, int S>
 __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
-                                          uint32_t sa, uint32_t sa_flags, uint32_t mlen) {
+                                          uint32_t sa, uint32_t sa_flags, uint32_t mlen,
+                                          uint4 *zs = nullptr, uint32_t zi = 0) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
   const int sep = (sa_flags & ESPGPU_CSP_F_SEPARATE_AAD) != 0;
@@ -755,9 +920,10 @@ __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds
   int Mw = M;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) Mw = max(Mw, __shfl_xor(Mw, o));
+  GCM_PHASE_T(8, true, kBurstCtrWaves * 64);
   const bool want_trl = DIR == 0 && p.trailer != nullptr;
   if (Mw == 0) {
-    if (have && l == 0 && !valid) {
+    if (zs == nullptr && have && l == 0 && !valid) {
       p.status[di] = ESPGPU_EINVAL;
       if (want_trl) p.trailer[di] = 0;
     }
@@ -770,21 +936,54 @@ __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds
     if (valid && i == N - 1) return make_uint4(0, bswap32(sep ? 96u : 64u), 0, bswap32((uint32_t)ct_len * 8));
     return make_uint4(0, 0, 0, 0);
   };
+  // lone-wave form for the burst kernel's S = 8 lanes
+  auto gmul = [&](uint4 v) { return S == kGcmLanesSmall ? gf_mul8_wide(v, lds, gl) : gf_mul8(v, lds, gl); };
   uint4 Y = make_uint4(0, 0, 0, 0);
+  // Small-batch lanes (S = 8) load their first kPre blocks (a 1500-byte
+  // packet's all) before the first multiply: a lone wave would otherwise wait
+  // a full load latency per step pair.
+  constexpr int kPre = S == kGcmLanesSmall ? 12 : 0;
+  uint4 Cp[kPre > 0 ? kPre : 1];
+#pragma unroll
+  for (int m = 0; m < kPre; ++m) {
+    const int i = S * m + l - pad;
+    Cp[m] = make_uint4(0, 0, 0, 0);
+    if (valid && m < M && i >= 1 && i <= nct) Cp[m] = ld16(rec + 16 * i);
+  }
+  GCM_PHASE_T(9, true, kBurstCtrWaves * 64);
   for (int m = 0; m < Mw; m += 2) {
     const int i = S * m + l - pad, ib = i + S;
     const bool two = m + 1 < Mw;                           // wave-uniform
     const bool la = valid && i >= 1 && i <= nct, lb = valid && two && ib >= 1 && ib <= nct;
     uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
-    if (la) Ca = ld16(rec + 16 * i);
-    if (lb) Cb = ld16(rec + 16 * ib);
+    if (kPre && m + 1 < kPre) {
+      // m is even: select the preloaded pair without dynamic register indexing
+#pragma unroll
+      for (int q = 0; q < kPre; q += 2)
+        if (q == m) {
+          Ca = Cp[q];
+          Cb = Cp[q + 1];
+        }
+    } else {
+      if (la) Ca = ld16(rec + 16 * i);
+      if (lb) Cb = ld16(rec + 16 * ib);
+    }
     const uint4 Ba = blk(i, la, Ca), Bb = blk(ib, lb, Cb);
-    const uint4 Ya = xor4(m == 0 ? Y : gf_mul8(Y, lds, gl), Ba);
+    const uint4 Ya = xor4(m == 0 ? Y : gmul(Y), Ba);
     if (m < M) Y = Ya;
     if (two) {
-      const uint4 Yb = xor4(gf_mul8(Y, lds, gl), Bb);
+      const uint4 Yb = xor4(gmul(Y), Bb);
       if (m + 1 < M) Y = Yb;
     }
+  }
+  GCM_PHASE_T(10, true, kBurstCtrWaves * 64);
+  if (zs != nullptr) {
+    uint4 Z = gf_mul4_global<S != kGcmLanesSmall>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+#pragma unroll
+    for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
+    if (have && l == 0) zs[zi] = Z;
+    GCM_PHASE_T(11, true, kBurstCtrWaves * 64);
+    return;
   }
   uint4 tag = make_uint4(0, 0, 0, 0), ej0 = make_uint4(0, 0, 0, 0);
   if (valid) {
@@ -800,7 +999,7 @@ __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds
       }
     }
   }
-  uint4 Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+  uint4 Z = gf_mul4_global<S != kGcmLanesSmall>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 T = xor4(Z, ej0);
@@ -817,6 +1016,33 @@ __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
     if (want_trl && !(valid && ok)) p.trailer[di] = 0;
   }
+}
+
+// The rest of tag_group for a record whose GHASH value Z is known (one thread
+// per record, burst kernel decrypt, after the ctr pass wrote E_K(J0) and the
+// trailer word): verify, status, trailer word zeroed on failure.
+__device__ __forceinline__ void tag_finish(const GcmParams &p, uint32_t di, uint32_t sa, uint32_t mlen, uint4 Z) {
+  const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+  const uint32_t len = dv.y & 0xffffu;
+  const int ct_len = (int)len - 16 - (int)mlen;
+  const bool valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
+  int ok = 0;
+  if (valid) {
+    const uint8_t *rec = p.arena + (size_t)dv.x * 4;
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(rec + len - mlen);
+    uint4 tag = make_uint4(0, 0, 0, 0);
+    if (mlen == 16) {
+      tag = ld16(rec + len - mlen);
+    } else {
+      tag.x = q[0];
+      tag.y = q[1];
+      if (mlen > 8) tag.z = q[2];
+    }
+    const uint4 d = mask_block(xor4(xor4(Z, p.ej0[di]), tag), (int)mlen);
+    ok = ((d.x | d.y | d.z | d.w) == 0);
+  }
+  p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+  if (p.trailer && !(valid && ok)) p.trailer[di] = 0;
 }
 
 // KIND 0: the ctr pass (S = kCtrLanes, T-table in LDS); KIND 1: the tag pass
@@ -908,15 +1134,55 @@ void gcm_split_kernel(GcmParams p) {
   }
 }
 
+// Self-staging prologue of one chunk (gcm_kernel<..., STAGE>): copies the
+// chunk's descriptors (p.hdesc -> p.desc) and records (p.xin) from host memory
+// through the mapping and keeps its result spans (p.xout) in LDS for the
+// epilogue.  Two dependent host reads per chunk: the spans and descriptor
+// words together, then every record's bytes at once (tpr threads per record,
+// one batch of loads each for records up to 2 KiB).
+template <int WG>
+__device__ __forceinline__ void stage_in(const GcmParams &p, uint32_t start, uint32_t count, XferSpan *s_xout) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t tpr = 64;                                    // threads per record: count x tpr <= WG
+  while (tpr > 1 && tpr * count > (uint32_t)WG) tpr >>= 1;
+  const uint32_t r = tid / tpr, sub = tid % tpr;
+  constexpr uint32_t kDW = sizeof(espgpu_desc) / 4;
+  static_assert(kChunkRecs * kDW <= 4 * WG, "descriptor words per thread");
+  const uint32_t nd = count * kDW;
+  const uint32_t *hd = reinterpret_cast<const uint32_t *>(p.hdesc + start);
+  uint32_t *dd = reinterpret_cast<uint32_t *>(const_cast<espgpu_desc *>(p.desc) + start);
+  uint32_t dv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (tid + k * WG < nd) dv[k] = hd[tid + k * WG];
+  XferSpan sp{0, 0, 0, 0}, so{0, 0, 0, 0};
+  if (r < count) {
+    sp = p.xin[start + r];
+    if (sub < 2) so = p.xout[2 * (start + r) + sub];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (tid + k * WG < nd) dd[tid + k * WG] = dv[k];
+  if (r < count) {
+    if (sub < 2) s_xout[2 * r + sub] = so;
+    xfer_copy<16>(sp.src, sp.dst, sp.len, sub, tpr);
+  }
+  __syncthreads();
+}
+
 // S lanes per record: kGcmLanesPerRec for throughput, kGcmLanesSmall for
 // batches too small to fill the chip (half the serial steps per record).
-template <int MODE, int WG, int S>
+// STAGE: the batch stages its own records (p.xin / p.xout, implicit chunks):
+// each chunk's records are copied in by the workgroup that runs the chunk and
+// its results copied out after it, so a burst is one launch.
+template <int MODE, int WG, int S, bool STAGE = false>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   static_assert(S == kGcmLanesPerRec || S == kGcmLanesSmall, "GHASH tables exist for these strides");
   constexpr int RPW = 64 / S;             // records per wave
   constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
+  GCM_PHASE(0, true);
 
   // T-table: per entry 32 slots of Te0 then 32 slots of Te1 (see tpa()).
   for (int idx = tid; idx < 256 * 32; idx += WG) {
@@ -925,6 +1191,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
     *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
     *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
   }
+  GCM_PHASE(1, true);
 
   const bool implicit = (p.chunks == nullptr);
   const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
@@ -936,15 +1203,19 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // s_ticket is double-buffered by iteration parity: slot it&1 is rewritten
   // only at it+2, after every thread passed iteration it+1's barrier.
   __shared__ uint32_t s_ticket[2];
+  __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
   for (uint32_t it = 0;; ++it) {
     if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
     __syncthreads();
     const uint32_t c = s_ticket[it & 1];
+    GCM_PHASE(2, it == 0);
     if (c >= nch) break;
     uint32_t sa, start, count;
     if (implicit) {
       start = c * p.chunk;
       count = min(p.chunk, p.n - start);
+      if (STAGE) stage_in<WG>(p, start, count, s_xout);
+      GCM_PHASE(3, it == 0);
       sa = p.desc[start].sa;
     } else {
       const Chunk ch = p.chunks[c];
@@ -973,6 +1244,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
       cur_sa = sa;
       __syncthreads();
     }
+    GCM_PHASE(4, it == 0);
     // a chunk takes kChunkRecs / (WG/8) passes of the workgroup
     for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * RPW) {
       const uint32_t rl = sub + (uint32_t)wave * RPW + (uint32_t)((tid & 63) / S);
@@ -997,7 +1269,27 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
       }
       do_group<MODE, S>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
     }
+    GCM_PHASE(5, it == 0);
+    if (STAGE) {
+      // statuses and the results of the records that passed back to the host
+      __syncthreads();
+      // (spans from LDS: no host read on the way out, the writes are posted)
+      for (uint32_t r = (uint32_t)wave; r < count; r += (uint32_t)(WG / 64)) {
+        const uint32_t di = start + r;
+        const uint8_t st = p.status[di];
+        if ((tid & 63) == 0) p.hstat[di] = st;
+        if (st == ESPGPU_OK) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const XferSpan sp = s_xout[2 * r + k];
+            if (sp.len) xfer_copy(sp.src, sp.dst, sp.len, (uint32_t)(tid & 63), 64u);
+          }
+        }
+      }
+      GCM_PHASE(6, it == 0);
+    }
   }
+  GCM_PHASE(7, true);
   // Every workgroup leaves the loop after drawing exactly one ticket >= nch,
   // so once all have retired no ticket is drawn again: reset for the next launch.
   if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
@@ -1006,7 +1298,177 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   }
 }
 
+// ---- burst kernel: the split design in one launch, for latency ----------------
+// A burst leaves the chip idle and the fused kernel's time is the serial chain
+// of each lane: S = 8 lanes walk a 1480-byte record in 12 AES + GHASH steps,
+// VALU-issue-bound in a lone wave (~7.7 K cycles per step pair, phase clock of
+// a 32-record burst, tools/burst_bench with the knobs library).  Here a chunk
+// runs the ctr pass with kBurstCtrLanes = 32 lanes per record (3 counter
+// blocks per lane) and the GHASH with kGcmLanesSmall = 8 lanes (12 multiplies,
+// the H^8 table), E_K(J0) handed over through p.ej0 as in the two-kernel split
+// design; both tables stay in LDS (T-table at LDS_TP, H^8 table at LDS_GT).
+// DIR 0, decrypt out of place: the GHASH of the ciphertext does not wait for
+// the ctr pass, so waves [0, kBurstCtrWaves) run the ctr pass while the others
+// hash (Z to LDS); after a barrier one thread per record verifies.
+// DIR 1, encrypt in place: the ctr pass, a barrier, then the tag pass over the
+// ciphertext it wrote (ICV, status).
+// STAGE: the batch stages its own records (stage_in / the epilogue, as
+// gcm_kernel<..., true>): one launch per burst.
+template <int DIR, int WG, bool STAGE = false>
+__global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
+  constexpr int ST = kGcmLanesSmall;
+  [[maybe_unused]] constexpr int S = ST;    // for the phase clock
+  GCM_PHASE(0, true);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < 256 * 32; idx += WG) {
+    const int x = idx >> 5, r = idx & 31;
+    const uint2 t = p.tpair[x];
+    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
+    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
+  }
+  GCM_PHASE(1, true);
+  const bool implicit = (p.chunks == nullptr);
+  const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
+  uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
+  const int wave = tid >> 6;
+  __shared__ uint4 s_z[DIR == 0 ? kChunkRecs : 1];
+  __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
+  __shared__ uint32_t s_ticket[2];
+  for (uint32_t it = 0;; ++it) {
+    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
+    __syncthreads();
+    const uint32_t c = s_ticket[it & 1];
+    GCM_PHASE(2, it == 0);
+    if (c >= nch) break;
+    uint32_t sa, start, count;
+    if (implicit) {
+      start = c * p.chunk;
+      count = min(p.chunk, p.n - start);
+      if (STAGE) stage_in<WG>(p, start, count, s_xout);
+      sa = p.desc[start].sa;
+    } else {
+      const Chunk ch = p.chunks[c];
+      sa = ch.sa;
+      start = ch.start;
+      count = ch.count;
+    }
+    sa = __builtin_amdgcn_readfirstlane(sa);
+    if (sa != cur_sa) {
+      __syncthreads();
+      if (sa < p.nsas) {
+        const DevSA *s = p.sas + sa;
+        nr = s->nr;
+        flags = s->flags;
+        mlen = s->mlen;
+        mode = s->mode;
+        if (mode == ESPGPU_CSP_MODE_AEAD) {
+          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + kGh8SmallOff);
+          uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
+#pragma unroll 4
+          for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+        }
+      } else {
+        mode = 0;
+      }
+      cur_sa = sa;
+      __syncthreads();
+    }
+    if (mode != ESPGPU_CSP_MODE_AEAD) {
+      // as gcm_kernel: EINVAL unless the ETA kernel's record
+      for (uint32_t r = (uint32_t)tid; r < count; r += WG) {
+        const uint32_t pos = start + r;
+        const uint32_t di = p.order ? p.order[pos] : pos;
+        const uint32_t rsa = p.desc[di].sa;
+        const bool eta = rsa < p.nsas && p.sas[rsa].mode == ESPGPU_CSP_MODE_ETA;
+        if (!eta) {
+          p.status[di] = ESPGPU_EINVAL;
+          if (DIR == 0 && p.trailer) p.trailer[di] = 0;
+        }
+      }
+      continue;
+    }
+    GCM_PHASE(3, it == 0);
+    const rkptr rk = (rkptr)(const void *)(p.sas[sa].rk);
+    constexpr uint32_t kCtrRpw = 64 / kBurstCtrLanes, kTagRpw = 64 / ST;
+    if (DIR == 0) {
+      constexpr uint32_t kCw = kBurstCtrWaves, kTw = WG / 64 - kBurstCtrWaves;
+      if ((uint32_t)wave < kCw) {
+        for (uint32_t sub = 0; sub < count; sub += kCw * kCtrRpw) {
+          const uint32_t rl = sub + (uint32_t)wave * kCtrRpw + (uint32_t)((tid & 63) / kBurstCtrLanes);
+          const bool have = rl < count;
+          const uint32_t pos = start + (have ? rl : 0);
+          const uint32_t di = p.order ? p.order[pos] : pos;
+          if (__any(have)) ctr_group<0, kBurstCtrLanes, true>(p, lds, di, have, sa, mlen, (int)nr, rk, LDS_TP);
+        }
+      } else {
+        for (uint32_t sub = 0; sub < count; sub += kTw * kTagRpw) {
+          const uint32_t rl = sub + ((uint32_t)wave - kCw) * kTagRpw + (uint32_t)((tid & 63) / ST);
+          const bool have = rl < count;
+          const uint32_t pos = start + (have ? rl : 0);
+          const uint32_t di = p.order ? p.order[pos] : pos;
+          if (__any(have)) tag_group<0, ST>(p, lds, di, have, sa, flags, mlen, s_z, rl);
+        }
+      }
+      GCM_PHASE(4, it == 0);
+      __syncthreads();
+      GCM_PHASE(5, it == 0);
+      for (uint32_t r = (uint32_t)tid; r < count; r += WG) {
+        const uint32_t pos = start + r;
+        tag_finish(p, p.order ? p.order[pos] : pos, sa, mlen, s_z[r]);
+      }
+      // s_z is rewritten by the next chunk's hash waves
+      __syncthreads();
+    } else {
+      for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * kCtrRpw) {
+        const uint32_t rl = sub + (uint32_t)wave * kCtrRpw + (uint32_t)((tid & 63) / kBurstCtrLanes);
+        const bool have = rl < count;
+        const uint32_t pos = start + (have ? rl : 0);
+        const uint32_t di = p.order ? p.order[pos] : pos;
+        if (__any(have)) ctr_group<1, kBurstCtrLanes, true>(p, lds, di, have, sa, mlen, (int)nr, rk, LDS_TP);
+      }
+      // the ciphertext and E_K(J0) written above are read below by other waves
+      __syncthreads();
+      for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * kTagRpw) {
+        const uint32_t rl = sub + (uint32_t)wave * kTagRpw + (uint32_t)((tid & 63) / ST);
+        const bool have = rl < count;
+        const uint32_t pos = start + (have ? rl : 0);
+        const uint32_t di = p.order ? p.order[pos] : pos;
+        if (__any(have)) tag_group<1, ST>(p, lds, di, have, sa, flags, mlen);
+      }
+    }
+    if (STAGE) {
+      // statuses and the results of the records that passed back to the host
+      __syncthreads();
+      for (uint32_t r = (uint32_t)wave; r < count; r += (uint32_t)(WG / 64)) {
+        const uint32_t di = start + r;
+        const uint8_t st = p.status[di];
+        if ((tid & 63) == 0) p.hstat[di] = st;
+        if (st == ESPGPU_OK) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const XferSpan sp = s_xout[2 * r + k];
+            if (sp.len) xfer_copy(sp.src, sp.dst, sp.len, (uint32_t)(tid & 63), 64u);
+          }
+        }
+      }
+    }
+    GCM_PHASE(6, it == 0);
+  }
+  GCM_PHASE(7, true);
+  if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
+    atomicExch(&p.queue[0], 0u);
+    atomicExch(&p.queue[1], 0u);
+  }
+}
+
 }  // namespace
+
+#ifdef ESPGPU_KNOBS
+extern "C" __attribute__((visibility("default"))) int espgpu_debug_phases(uint64_t *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int set_gcm_opts(uint32_t opts) {
 #ifdef ESPGPU_KNOBS
@@ -1038,7 +1500,7 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   constexpr int W = kGcmLanesSmall;
-  const bool small = lanes ? lanes == W : pp.n < kGcmSmallBatch;
+  const bool small = pp.xin != nullptr || (lanes ? lanes == W : pp.n < kGcmSmallBatch);
   GcmParams p = pp;
   // implicit chunks (caller-grouped batch): kChunkRecs records each, or for a
   // batch of fewer than grid x kChunkRecs records as few as four waves'
@@ -1049,14 +1511,38 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
   // only fill LDS and leave)
   // Chunk sizes are powers of two, so every chunk lies inside one aligned run
   // of kChunkRecs records (the grouping contract, include/espgpu.h).
-  const uint32_t rpw = 64 / (small ? W : kGcmLanesPerRec), per = (pp.n + (uint32_t)grid - 1) / (uint32_t)grid;
-  p.chunk = 4 * rpw;
+  // burst kernel (small, E_K(J0) scratch given, out of place or encrypt):
+  // chunks of one ctr wave's records, so a burst spreads over CUs
+  const bool burst = small && pp.ej0 != nullptr && !two_pass;
+  const uint32_t rpw = burst ? 64 / kCtrLanes : 64 / (small ? W : kGcmLanesPerRec);
+  const uint32_t per = (pp.n + (uint32_t)grid - 1) / (uint32_t)grid;
+  p.chunk = (small && !burst ? GCM_SMALL_CHUNK_WAVES : burst ? 1 : 4) * rpw;
   while (p.chunk < per && p.chunk < (uint32_t)kChunkRecs) p.chunk <<= 1;
 #if GCM_WG != 1024
   if (!small) p.chunk = (GCM_WG / 64) * (64 / kGcmLanesPerRec);   // experiment: one pass per chunk
 #endif
   if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + p.chunk - 1) / p.chunk)));
   if (!small && p.ej0 != nullptr) return launch_gcm_split(p, encrypt, two_pass, grid, st);
+  if (burst) {
+    if (p.xin != nullptr && p.chunks != nullptr) return -1;   // self-staging: implicit chunks only
+    if (p.xin != nullptr && encrypt)
+      hipLaunchKernelGGL((gcm_burst_kernel<1, kBurstWG, true>), dim3(grid), dim3(kBurstWG), 0, st, p);
+    else if (p.xin != nullptr)
+      hipLaunchKernelGGL((gcm_burst_kernel<0, kBurstWG, true>), dim3(grid), dim3(kBurstWG), 0, st, p);
+    else if (encrypt)
+      hipLaunchKernelGGL((gcm_burst_kernel<1, kBurstWG>), dim3(grid), dim3(kBurstWG), 0, st, p);
+    else
+      hipLaunchKernelGGL((gcm_burst_kernel<0, kBurstWG>), dim3(grid), dim3(kBurstWG), 0, st, p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  if (p.xin != nullptr) {   // self-staging small batch (implicit chunks, S = 8, never in place)
+    if (p.chunks != nullptr || two_pass) return -1;
+    if (encrypt)
+      hipLaunchKernelGGL((gcm_kernel<1, 1024, W, true>), dim3(grid), dim3(1024), 0, st, p);
+    else
+      hipLaunchKernelGGL((gcm_kernel<0, 1024, W, true>), dim3(grid), dim3(1024), 0, st, p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (small) {
     if (encrypt)
       hipLaunchKernelGGL((gcm_kernel<1, 1024, W>), dim3(grid), dim3(1024), 0, st, p);

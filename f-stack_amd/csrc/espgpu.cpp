@@ -27,6 +27,9 @@ using namespace espgpu;
 
 namespace {
 
+#ifndef GCM_BURST_DEFAULT
+#define GCM_BURST_DEFAULT 4096
+#endif
 #ifndef GPU_TIME_SMALL
 #define GPU_TIME_SMALL 0
 #endif
@@ -171,6 +174,8 @@ struct espgpu_ctx {
   Overflow ovf;
   size_t ovf_cap = 0;            // set_tuning "overflow_mb" (0: ERESTART when the slots are busy)
   int xfer_small = 1;            // small batches: staging region moved by the xfer kernel (else hipMemcpyAsync)
+  int stage_fused = 1;           // small single-session GCM batches stage their own records (one launch)
+  uint32_t gcm_burst = GCM_BURST_DEFAULT;   // small GCM batches of <= this many records: burst kernel
   std::vector<HostRegion> regions;   // sorted by base
   // completions not yet handed to poll(): ready[ready_head..] (host-side
   // rejects and finished batches), reserved so steady state does not allocate
@@ -350,9 +355,17 @@ bool slot_full(const espgpu_ctx *c, const Slot &s, int op, uint32_t rlen) {
 // Launch the crypto kernels for one batch of device-resident records.
 // kinds: which kernels the batch needs (1 GCM, 2 ETA); the device-resident
 // entry points do not know and pass both.
+// The self-staging lists of a small single-session GCM process batch
+// (GcmParams::xin / xout / hstat).
+struct StageLists {
+  const XferSpan *xin, *xout;
+  uint8_t *hstat;
+  const espgpu_desc *hdesc;
+};
+
 int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
               uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st,
-              uint32_t *d_trailer = nullptr, uint32_t kinds = 3) {
+              uint32_t *d_trailer = nullptr, uint32_t kinds = 3, const StageLists *stage = nullptr) {
   if (n == 0) return 0;
   if (c->launched && st != c->last_st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
   const uint32_t nsas = (uint32_t)c->sessions.size();
@@ -368,6 +381,12 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   p.nsas = nsas;
   p.queue = c->d_queue;
   p.trailer = encrypt ? nullptr : d_trailer;
+  if (stage) {
+    p.xin = stage->xin;
+    p.xout = stage->xout;
+    p.hstat = stage->hstat;
+    p.hdesc = stage->hdesc;
+  }
   if (!(flags & ESPGPU_BATCH_GROUPED)) {
     int e = ensure_plan(c, n);
     if (e) return e;
@@ -379,7 +398,11 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  if ((kinds & 1) && c->gcm_split && (c->gcm_lanes == kGcmLanesPerRec || (c->gcm_lanes == 0 && n >= kGcmSmallBatch))) {
+  // E_K(J0) scratch: the split design (large batches, set_tuning gcm_split) and
+  // the burst kernel (small batches of <= gcm_burst records, out of place or
+  // encrypt; launch_gcm picks the kernel from it)
+  const bool gsmall = c->gcm_lanes ? c->gcm_lanes == kGcmLanesSmall : n < kGcmSmallBatch;
+  if ((kinds & 1) && ((c->gcm_split && !gsmall) || (gsmall && !two_pass && n <= c->gcm_burst))) {
     if (n > c->ej0_cap) {
       hipFree(c->d_ej0);
       c->d_ej0 = nullptr;
@@ -884,6 +907,55 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
   hipStream_t s_k = small ? s.st : c->stream;
   hipStream_t s_in = small ? s.st : c->s_in, s_out = small ? s.st : c->s_out;
   uint8_t *dres = s.op ? s.d_arena : s.d_out;      // records out: in place (encrypt) or d_out
+  // A small batch of one GCM session stages its own records: the kernel's
+  // workgroups copy each chunk's records in from the host (pinned staging or
+  // registered memory) and the results back, reading the descriptors and
+  // writing the statuses through the host mapping -- one launch per burst
+  // instead of copy, kernel, copy (set_tuning "stage_fused"; the small-batch
+  // GCM kernel, so not with gcm_lanes 4 or gcm_split forced)
+  if (small && c->stage_fused && !s.mixed && s.kinds == 1 && c->gcm_lanes != kGcmLanesPerRec && !c->gcm_split) {
+    const uint32_t need = 3 * s.nrec;
+    if (need > s.xfer_cap) {
+      hipHostFree(s.h_xfer);
+      s.h_xfer = nullptr;
+      s.xfer_cap = 0;
+      const uint32_t cap = std::max(need, 256u) * 2;
+      HIPCHK(c, hipHostMalloc((void **)&s.h_xfer, (size_t)cap * sizeof(XferSpan), hipHostMallocDefault));
+      HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_xfer_dev, s.h_xfer, 0));
+      s.xfer_cap = cap;
+    }
+    const uint64_t ha = (uint64_t)(uintptr_t)s.h_arena_dev, da = (uint64_t)(uintptr_t)s.d_arena;
+    const uint64_t dr = (uint64_t)(uintptr_t)dres;
+    XferSpan *xin = s.h_xfer, *xout = s.h_xfer + s.nrec;
+    for (const Pending &pd : s.reqs) {
+      xin[pd.rec] = XferSpan{pd.zc ? pd.zc : ha + pd.stage_off, da + pd.stage_off, pd.stage_len, pd.rec};
+      for (int q = 0; q < 2; ++q) {
+        XferSpan &o = xout[2 * pd.rec + q];
+        if (q < pd.nspan) {
+          const Pending::Span &sp = pd.span[q];
+          o = XferSpan{dr + pd.stage_off + sp.stage_from,
+                       pd.zc ? pd.zc + sp.stage_from : ha + pd.stage_off + sp.stage_from, sp.n, pd.rec};
+        } else {
+          o = XferSpan{0, 0, 0, pd.rec};
+        }
+      }
+    }
+    const StageLists stg{s.h_xfer_dev, s.h_xfer_dev + s.nrec, s.h_arena_dev + s.stat_off,
+                         reinterpret_cast<const espgpu_desc *>(s.h_arena_dev + s.desc_off)};
+    s.timed = GPU_TIME_SMALL;
+    if (s.timed) hipEventRecord(s.k0, s_k);
+    int e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
+                      dres + s.stat_off, s.op ? nullptr : s.d_out, (uint32_t)ESPGPU_BATCH_GROUPED, s.op, s_k,
+                      nullptr, 1u, &stg);
+    if (e) return e;
+    if (s.timed) hipEventRecord(s.k1, s_k);
+    HIPCHK(c, hipEventRecord(s.done, s_k));
+    s.state = SLOT_INFLIGHT;
+    c->stats.batches++;
+    c->stats.zerocopy += s.nrec - s.nstaged;
+    c->cur = (c->cur + 1) % (int)c->slots.size();
+    return 0;
+  }
   // region the copies move: all of it, or without records if every one is zero-copy
   const uint32_t in_lo = s.nstaged ? 0 : s.desc_off, out_lo = s.nstaged ? 0 : s.stat_off;
   const uint32_t out_hi = s.stat_off + s.nrec;
@@ -1274,6 +1346,16 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
     c->ovf.bytes.reserve(rb);
     c->ovf.ent.reserve(re);
     c->ovf.segpool.reserve(re);
+    return 0;
+  }
+  if (!strcmp(key, "gcm_burst")) {
+    if (value < 0) return ESPGPU_EINVAL;
+    c->gcm_burst = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "stage_fused")) {
+    if (value != 0 && value != 1) return ESPGPU_EINVAL;
+    c->stage_fused = value;
     return 0;
   }
   if (!strcmp(key, "xfer")) {

@@ -87,6 +87,16 @@ struct GcmParams {
   uint32_t *trailer;              // decrypt: fused esp_input_cb trailer words, or nullptr
   uint32_t chunk;                 // implicit mode: records per chunk (launch_gcm sets it)
   uint4 *ej0;                     // split design: E_K(J0) per descriptor (nullptr: fused kernel)
+  // A small single-session process batch that stages its own records (one
+  // kernel instead of copy, kernel, copy): per descriptor i, xin[i] copies the
+  // record into the arena before its chunk runs and xout[2i], xout[2i+1] copy
+  // its results back after (len 0: none; only if its status is 0); hstat is
+  // the host status array; hdesc the host descriptors, which each chunk
+  // copies to desc (device) with its records.  nullptr: the records are in
+  // the arena already.
+  const struct XferSpan *xin, *xout;
+  uint8_t *hstat;
+  const espgpu_desc *hdesc;
 };
 
 struct EtaParams {

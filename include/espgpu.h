@@ -338,6 +338,13 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *               in flight, in MiB (0, the default: ERESTART; 0..65536);
  *   "xfer"      small batches' staging region moved by the xfer kernel (1,
  *               default) or by hipMemcpyAsync (0);
+ *   "gcm_burst" GCM batches of up to this many records (default 4096) that
+ *               run the small-batch design, out of place or encrypt, use the
+ *               burst kernel (a 32-lane CTR pass and an 8-lane GHASH in one
+ *               launch, for latency); 0 = the fused small-batch kernel;
+ *   "stage_fused" a process-path burst of one GCM session stages its own
+ *               records inside the crypto kernel (1, default: one launch per
+ *               burst) instead of xfer kernels around it (0);
  *   "gcm_opts" / "eta_opts" measurement knobs that skip work on purpose
  *               (results wrong): only in libespgpu_knobs.so, ENOTSUP in the
  *               product library unless 0.

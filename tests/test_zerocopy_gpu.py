@@ -277,3 +277,63 @@ def test_overflow_cap_then_erestart():
             assert bytes(pkts[i]) == bytes(ct[o:o + L])
     finally:
         drv.close()
+
+
+@pytest.mark.parametrize("fused", [1, 0], ids=["self-staging", "xfer"])
+@pytest.mark.parametrize("burst", [4096, 0], ids=["burst-kernel", "fused-kernel"])
+@pytest.mark.parametrize("esn", [False, True])
+def test_single_session_gcm_burst_self_staging(fused, burst, esn):
+    """A small single-session GCM batch stages its own records (set_tuning
+    "stage_fused"): the kernel's workgroups copy each chunk's records in (from
+    registered memory at any alignment, or the pinned staging buffer), read
+    the descriptors and write the statuses through the host mapping, and copy
+    the results of the records that passed back.  Encrypt and tampered decrypt
+    vs the oracle, against the xfer-kernel path (fused 0); through the burst
+    kernel (gcm_burst, the default for these sizes) and the fused small-batch
+    kernel (gcm_burst 0)."""
+    from espgpu.esp import esp_input_crp, esp_output_crp
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=4)
+    try:
+        assert drv.set_tuning("stage_fused", fused) == 0
+        assert drv.set_tuning("gcm_burst", burst) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2500 + fused + 2 * esn)
+        sas = [GcmSA(rng, 16 if not esn else 32, esn=esn, mlen=16 if not esn else 12)]
+        err, cs = fw.crypto_newsession(sas[0].esp_sa().csp())
+        assert err == 0
+        for n in (1, 32, 77):
+            idx = np.zeros(n, dtype=np.int64)
+            eh = rng.integers(0, 2**32, n, dtype=np.uint32)
+            plain, ct, descs, eh = build_records(rng, sas, idx, rng.choice([4, 12, 100, 1448], n), esn_hi=eh)
+            reg = np.zeros(1 << 18, dtype=np.uint8)
+            drv.register_host(reg)
+            lay = _Layout(rng, descs, n, reg, frac_reg=0.6)
+            sa = sas[0].esp_sa()
+            for i in range(n):
+                lay.put(i, plain)
+            crps = [esp_output_crp(fw, cs, sa, lay.pkt(i), lay.skip, esn_hi=int(eh[i])) for i in range(n)]
+            _run(fw, crps)
+            for i in range(n):
+                o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+                assert crps[i].crp_etype == 0 and lay.get(i) == bytes(ct[o:o + L]), (n, i)
+            bad = set(int(i) for i in rng.choice(n, max(1, n // 8), replace=False))
+            before = {}
+            for i in range(n):
+                lay.put(i, ct)
+                if i in bad:
+                    lay.pkt(i)[lay.skip + int(descs["len"][i]) - 2] ^= 0x01
+                    before[i] = lay.get(i)
+            crps = [esp_input_crp(fw, cs, sa, lay.pkt(i), lay.skip, esn_hi=int(eh[i])) for i in range(n)]
+            _run(fw, crps)
+            for i in range(n):
+                o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+                if i in bad:
+                    assert crps[i].crp_etype == O.EBADMSG and lay.get(i) == before[i], (n, i)
+                else:
+                    assert crps[i].crp_etype == 0, (n, i)
+                    assert lay.get(i)[16:L - sa.mlen] == bytes(plain[o + 16:o + L - sa.mlen]), (n, i)
+            drv.unregister_host(reg)
+        fw.crypto_freesession(cs)
+    finally:
+        drv.close()

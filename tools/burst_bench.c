@@ -35,6 +35,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <dlfcn.h>
 
 #include "espgpu.h"
 
@@ -252,6 +253,20 @@ int main(int argc, char **argv)
 					if (it >= 0) lat[it] = now_us() - t0;
 				}
 				const int bad_latency = bad;
+				/* knobs library only: the small GCM kernel's phase clock of the
+				 * last latency burst (workgroup 0, first chunk) */
+				int (*phases)(unsigned long long *) =
+					(int (*)(unsigned long long *))dlsym(RTLD_DEFAULT, "espgpu_debug_phases");
+				unsigned long long ph[32];
+				if (phases && phases(ph) == 0) {
+					printf("{\"phases\": %d, \"mode\": %d, \"xfer\": %d, \"clk\": [", B, mode, xfer);
+					for (int k = 1; k < 12; k++)
+						printf("%s%lld", k > 1 ? ", " : "", (long long)(ph[2 * k] - ph[0]));
+					printf("], \"real_10ns\": [");
+					for (int k = 1; k < 12; k++)
+						printf("%s%lld", k > 1 ? ", " : "", (long long)(ph[2 * k + 1] - ph[1]));
+					printf("]}\n");
+				}
 				qsort(lat, iters, sizeof(double), cmp_d);
 				const double med = lat[iters / 2], p99 = lat[(int)(iters * 0.99)];
 				double wp;
