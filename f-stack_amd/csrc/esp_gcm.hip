@@ -44,6 +44,7 @@
 
 #include <algorithm>
 
+#include "aes_bs.h"
 #include "espgpu_internal.h"
 #include "xfer_copy.h"
 
@@ -62,6 +63,9 @@
 #endif
 #ifndef GCM_CTR_SINGLE
 #define GCM_CTR_SINGLE 0
+#endif
+#ifndef GCM_BS_VGPRS
+#define GCM_BS_VGPRS 192
 #endif
 #ifndef GCM_SPLIT_WPE
 #define GCM_SPLIT_WPE 4
@@ -183,7 +187,8 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
 // tools/gcm_timing.py --opts, bench.py --tuning gcm_opts=N): bit0 skips the
 // record loads and plaintext stores, bit1 the GHASH multiplies, bit2 the AES
 // rounds after round 2, bit3 the stores only, bit4 the loads only, bit5 the
-// per-session GHASH table staging, bit6 the per-record final multiply.  They break results on purpose, to split
+// per-session GHASH table staging, bit6 the per-record final multiply; bitsliced ctr pass: bit7 the AES
+// rounds but the last, bit8 the memory side (DMA, stores), bit9 the transposes.  They break results on purpose, to split
 // the kernel's time between memory, GHASH, AES and per-session setup.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t g_opts;
@@ -831,7 +836,7 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
       rec = p.arena + (size_t)dv.x * 4;
       const uint4 h = ld16(rec);
       nct = (ct_len + 15) >> 4;
-      K = DIR == 3 ? 1 : (nct + S) / S;                    // J0 + nct blocks over S lanes
+      K = DIR >= 3 ? 1 : (nct + S) / S;                    // J0 + nct blocks over S lanes
       s0c = bswap32(dv.w) ^ rk[0];
       s1c = bswap32(h.z) ^ rk[1];
       s2c = bswap32(h.w) ^ rk[2];
@@ -841,7 +846,7 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) Kw = max(Kw, __shfl_xor(Kw, o));
   if (Kw == 0) return;
-  const bool want_trl = (DIR == 0 || DIR == 2) && p.trailer != nullptr;
+  const bool want_trl = (DIR == 0 || DIR == 2 || DIR == 4) && p.trailer != nullptr;
   uint8_t *orec = DIR == 0 ? p.out - p.arena + rec : rec;
   const uint32_t rk3 = rk[3];
   CtrCache cc;
@@ -856,16 +861,18 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
     if (!loaded) return;
     const int rem = ct_len - 16 * i;
     const uint4 o = xor4(C, ks);
-    st_partial(orec + 16 + 16 * i, o, rem);
+    if (DIR != 4) st_partial(orec + 16 + 16 * i, o, rem);
     if (want_trl && i == nct - 1)
       p.trailer[di] = esp_trailer_word(rem >= 16 ? o.w : (rem > 8 ? o.z : (rem > 4 ? o.y : o.x)),
                                        (uint32_t)ct_len);
   };
   for (int k = 0; k < Kw; k += 2) {
-    const int ia = l - 1 + S * k, ib = ia + S;
+    // DIR 4 (pre pass of the concurrent bitsliced design): lane 0 E_K(J0),
+    // lane 1 the last ciphertext block (the trailer word), nothing stored
+    const int ia = DIR == 4 ? (l == 0 ? -1 : (l == 1 ? nct - 1 : -2)) : l - 1 + S * k, ib = ia + S;
     const bool two = k + 1 < Kw;                           // wave-uniform
     const bool la = DIR != 3 && valid && ia >= 0 && ia < nct;
-    const bool lb = DIR != 3 && valid && two && ib < nct;
+    const bool lb = DIR != 3 && DIR != 4 && valid && two && ib < nct;
     uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
     if (la) Ca = ld16(rec + 16 + 16 * ia);
     if (lb) Cb = ld16(rec + 16 + 16 * ib);
@@ -1123,7 +1130,7 @@ void gcm_split_kernel(GcmParams p) {
         continue;
       }
       if (KIND == 0)
-        ctr_group<DIR>(p, lds, di, have, sa, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
+        ctr_group<DIR, S>(p, lds, di, have, sa, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
       else
         tag_group<DIR, S>(p, lds, di, have, sa, flags, mlen);
     }
@@ -1462,6 +1469,271 @@ __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
   }
 }
 
+// ---- bitsliced ctr pass (aes_bs.h) -------------------------------------------
+// The split design's ctr pass with the AES on the VALU instead of the LDS
+// (the T-table kernels are bound by the LDS lookup rate).  A
+// lane owns a WINDOW of 32 consecutive counters of one record (window w:
+// counters 32w .. 32w+31; CT block c has counter c + 2) and encrypts them
+// bitsliced, 32 blocks per register bit.  A chunk's windows are numbered by a
+// prefix sum over its records (a 1500-byte record has 3) and each thread takes
+// one.  After the rounds a 32x32 bit transpose per state word turns the
+// keystream into blocks, which the lane XORs into its own window's blocks.
+// The window's ciphertext comes into LDS by LDS-DMA (global_load_lds, no
+// VGPRs), a quarter (8 blocks) at a time in two buffers: quarters 0 and 1 are
+// requested before the rounds, so their latency hides under the AES; DMA
+// instruction k writes block k of every lane's window at k*1 KiB + lane*16,
+// which is also where the lane reads it back (conflict-free ds_read_b128).
+// DIR 0: decrypt out of place; SEQ: also E_K(J0) and the trailer word, for the
+//        tag pass that follows on the same stream (otherwise the concurrent
+//        design's pre pass, ctr_group<4>, writes them);
+// DIR 1: encrypt in place, E_K(J0) for the tag pass that follows;
+// DIR 2: decrypt in place the records whose status is OK (verify-first), with
+//        the trailer word.
+// Session keys: DevSA::dk of an AEAD session = K0, K'_1 .. K'_nr as
+// little-endian words with K'_r = K_r ^ 0x63..63 (aes_bs.h).
+constexpr int kBsWG = 256;                 // one wave per SIMD; two workgroups per CU
+constexpr uint32_t kBsQuarter = 8 * 64 * 16;   // LDS bytes of one quarter buffer (8 blocks x 64 windows)
+
+// 32x32 bit transpose: afterwards bit i of a[s] = bit s of the old a[i]
+// (swapmove ladder; the 16- and 8-bit stages are byte moves)
+__device__ __forceinline__ void bs_transpose32(uint32_t *a) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t x = a[k], y = a[k + 16];
+    a[k] = perm(y, x, 0x05040100u);
+    a[k + 16] = perm(y, x, 0x07060302u);
+  }
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if (k & 8) continue;
+    const uint32_t x = a[k], y = a[k + 8];
+    a[k] = perm(y, x, 0x06020400u);
+    a[k + 8] = perm(y, x, 0x07030501u);
+  }
+  constexpr uint32_t M[3] = {0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int j = 4 >> q;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      if (k & j) continue;
+      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & M[q];
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
+}
+
+template <int DIR, bool SEQ>
+__global__ __launch_bounds__(kBsWG) __attribute__((amdgpu_waves_per_eu(2), amdgpu_num_vgpr(GCM_BS_VGPRS)))
+void gcm_bsctr_kernel(GcmParams p) {
+  constexpr int NW = kBsWG / 64;
+  __shared__ __attribute__((aligned(16))) uint8_t s_ct[NW][2][kBsQuarter];   // ciphertext quarters, two buffers
+  __shared__ uint4 s_own[NW][64];     // the lane's window across the rounds: rec offset/4, ct_len, w, di
+  __shared__ uint32_t s_incl[kChunkRecs];
+  __shared__ uint32_t s_wsum[NW];
+  __shared__ uint32_t s_ticket[2];
+  static_assert(kChunkRecs == NW * 64, "one record per thread in the window scan");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS-DMA bases in SGPRs
+  const bool implicit = (p.chunks == nullptr);
+  const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
+  const bool want_trl = (DIR == 2 || (DIR == 0 && SEQ)) && p.trailer != nullptr;
+  for (uint32_t it = 0;; ++it) {
+    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
+    __syncthreads();
+    const uint32_t c = s_ticket[it & 1];
+    if (c >= nch) break;
+    uint32_t sa, start, count;
+    if (implicit) {
+      start = c * p.chunk;
+      count = min(p.chunk, p.n - start);
+      sa = p.desc[start].sa;
+    } else {
+      const Chunk ch = p.chunks[c];
+      sa = ch.sa;
+      start = ch.start;
+      count = ch.count;
+    }
+    sa = __builtin_amdgcn_readfirstlane(sa);
+    const bool aead = sa < p.nsas && p.sas[sa].mode == ESPGPU_CSP_MODE_AEAD;
+    const uint32_t mlen = aead ? p.sas[sa].mlen : 16u;
+    // windows per record (0 for a record this pass does not touch; the tag
+    // pass owns every status)
+    uint32_t nw = 0;
+    if (aead && (uint32_t)tid < count) {
+      const uint32_t pos = start + (uint32_t)tid;
+      const uint32_t di = p.order ? p.order[pos] : pos;
+      const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+      const uint32_t len = dv.y & 0xffffu;
+      const int ct_len = (int)len - 16 - (int)mlen;
+      bool valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
+      if (DIR == 2 && valid) valid = p.status[di] == ESPGPU_OK;
+      if (valid) nw = ((((uint32_t)ct_len + 15) >> 4) + 1 >> 5) + 1;   // counters 2 .. nct+1
+    }
+    uint32_t v = nw;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(v, o);
+      if (lane >= o) v += u;
+    }
+    if (lane == 63) s_wsum[wave] = v;
+    __syncthreads();
+    for (int k = 0; k < wave; ++k) v += s_wsum[k];
+    s_incl[tid] = v;
+    __syncthreads();
+    const uint32_t total = s_incl[kChunkRecs - 1];
+    const rkptr K = (rkptr)(const void *)(p.sas[aead ? sa : 0].dk);
+    const int nr = aead ? (int)p.sas[sa].nr : 0;
+    for (uint32_t base = 0; base < total; base += kBsWG) {
+      const uint32_t gw = base + (uint32_t)tid;
+      const bool has = gw < total;
+      if (!__any(has)) break;                         // wave-uniform: the tail pass
+      // owner record: the number of records whose inclusive count is <= gw
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t step = kChunkRecs / 2; step; step >>= 1)
+        if (s_incl[r + step - 1] <= gw) r += step;
+      uint32_t di = 0, roff = 0, ctl = 0, w = 0, W0 = 0, W1 = 0, W2 = 0;
+      if (has) {
+        w = gw - (r ? s_incl[r - 1] : 0u);
+        const uint32_t pos = start + r;
+        di = p.order ? p.order[pos] : pos;
+        const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
+        ctl = (dv.y & 0xffffu) - 16u - mlen;
+        roff = dv.x;
+        const uint4 h = ld16(p.arena + (size_t)roff * 4);
+        W0 = dv.w;                                    // salt
+        W1 = h.z;                                     // explicit IV
+        W2 = h.w;
+      }
+      // this lane's window: blocks cb = 32w + s - 2 of the record, s = 0..31;
+      // kept in LDS across the rounds (registers there hold the AES state)
+      s_own[wave][lane] = make_uint4(roff, has ? ctl : 0u, w, di);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      // Quarter buffer layout: window o's block k at o*128 + ((k - o) & 7)*16.
+      // In DMA / store instruction i, lanes 8m..8m+7 move window 8i + m's
+      // 128 contiguous bytes (block (j + o) & 7 on lane 8m + j, lane-linear in
+      // LDS at i*1 KiB + lane*16); the owner lane reads and writes its blocks
+      // across the 16 bank quads instead of one.
+      auto dma_quarter = [&](int q) {
+        uint8_t *buf = &s_ct[wave][q & 1][0];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int o = 8 * i + (lane >> 3);
+          const uint4 ow = s_own[wave][o];
+          const int cb = 32 * (int)ow.z + 8 * q + ((lane + o) & 7) - 2;
+          if (cb >= 0 && cb < (int)((ow.y + 15) >> 4))
+            __builtin_amdgcn_global_load_lds(p.arena + (size_t)ow.x * 4 + 16 + 16 * cb,
+                                             (__attribute__((address_space(3))) void *)(buf + i * 1024), 16, 0, 0);
+          if (i & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      if (!(gopts() & 256)) {
+        dma_quarter(0);
+        dma_quarter(1);
+      }
+      // bitsliced counter blocks salt || IV || BE32(32w + s), s = bit index
+      uint32_t st[128];
+      const uint32_t W3 = bswap32(32u * w);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t word = j < 4 ? W0 : j < 8 ? W1 : j < 12 ? W2 : W3;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          st[8 * j + b] = (uint32_t)((int32_t)(word << (31 - (8 * (j & 3) + b))) >> 31);
+      }
+      st[120] = 0xAAAAAAAAu;                          // counter bits 0..4 = the slice
+      st[121] = 0xCCCCCCCCu;
+      st[122] = 0xF0F0F0F0u;
+      st[123] = 0xFF00FF00u;
+      st[124] = 0xFFFF0000u;
+#pragma unroll 1
+      for (int rr = 0; rr < ((gopts() & 128) ? 0 : nr - 1); ++rr) {
+        const uint32_t k[4] = {K[4 * rr], K[4 * rr + 1], K[4 * rr + 2], K[4 * rr + 3]};
+        bs::round<true>(st, k);
+      }
+      {
+        const uint32_t k[4] = {K[4 * nr - 4], K[4 * nr - 3], K[4 * nr - 2], K[4 * nr - 1]};
+        bs::round<false>(st, k);
+      }
+      // keystream blocks: word g of slice s -> st[32g + s], last round key added
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (!(gopts() & 512)) bs_transpose32(&st[32 * g]);
+        const uint32_t kl = K[4 * nr + g];
+#pragma unroll
+        for (int s = 0; s < 32; ++s) st[32 * g + s] ^= kl;
+      }
+      if (DIR == 1 || SEQ) {                          // slice 1 = counter 1 = J0
+        const uint4 o = s_own[wave][lane];
+        if (o.y != 0 && o.z == 0) p.ej0[o.w] = make_uint4(st[1], st[33], st[65], st[97]);
+      }
+      // quarters 0 and 1 (requested before the rounds), then 2 and 3 into the
+      // same two buffers once they are read
+      const uint4 own = s_own[wave][lane];
+      const uint32_t ctl2 = (gopts() & 256) ? 0u : own.y;
+      const int nct = (int)((ctl2 + 15) >> 4);
+      uint8_t *const obase = (DIR == 0 ? p.out : p.arena) + 16;
+      // rolled over the quarters: quarter q's keystream is always st[8 blocks
+      // at 32g .. 32g+7] and the state shifts down 8 blocks per quarter, so
+      // one loop body serves all four
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        if (q == 0 || q == 2) __builtin_amdgcn_s_waitcnt(0x0f70);          // vmcnt(0)
+        uint8_t *buf = &s_ct[wave][q & 1][0];
+        // owner: its 8 blocks of this quarter, ciphertext -> result in place
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int cb = 32 * (int)own.z + 8 * q + k - 2, sl = k;
+          if (cb >= 0 && cb < nct) {
+            uint4 *slot = reinterpret_cast<uint4 *>(buf + lane * 128 + ((k - lane) & 7) * 16);
+            const uint4 o4 = xor4(*slot, make_uint4(st[sl], st[32 + sl], st[64 + sl], st[96 + sl]));
+            *slot = o4;
+            const int rem = (int)ctl2 - 16 * cb;
+            if (want_trl && cb == nct - 1)
+              p.trailer[own.w] = esp_trailer_word(rem >= 16 ? o4.w : (rem > 8 ? o4.z : (rem > 4 ? o4.y : o4.x)), ctl2);
+          }
+          // one block at a time: hoisting the reads would hold them beside
+          // the 128 keystream registers
+          if (k & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        // stores: 128 contiguous bytes per 8 lanes
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int o = 8 * i + (lane >> 3);
+          const uint4 ow = s_own[wave][o];
+          const int len = (gopts() & 256) ? 0 : (int)ow.y;
+          const int cb = 32 * (int)ow.z + 8 * q + ((lane + o) & 7) - 2;
+          if (cb >= 0 && cb < ((len + 15) >> 4))
+            st_partial(obase + (size_t)ow.x * 4 + 16 * cb, *reinterpret_cast<const uint4 *>(buf + i * 1024 + lane * 16),
+                       len - 16 * cb);
+          if (i & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        if (q == 1) {
+          // both buffers read (lgkmcnt 0) before the DMA overwrites them
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          dma_quarter(2);
+          dma_quarter(3);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 24; ++j) st[32 * g + j] = st[32 * g + j + 8];
+      }
+    }
+    // s_incl / s_own are rewritten by the next chunk
+    __syncthreads();
+  }
+  if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
+    atomicExch(&p.queue[0], 0u);
+    atomicExch(&p.queue[1], 0u);
+  }
+}
+
 }  // namespace
 
 #ifdef ESPGPU_KNOBS
@@ -1496,7 +1768,44 @@ static int launch_gcm_split(const GcmParams &p, int encrypt, int two_pass, int g
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream) {
+// The bitsliced ctr pass (gcm_bsctr_kernel, its own ticket counters at
+// queue[4..5]) with the T-table tag pass.  bs.mode 1: one stream, ctr pass
+// then tag pass (the split design's order); bs.mode 2, decrypt out of place:
+// the ctr pass on `st` and, at the same time on bs.aux, the pre pass
+// (ctr_group<4>: E_K(J0) and the trailer word, two lanes per record) then the
+// tag pass, both in one-wave-per-SIMD workgroups so that they fit on every CU
+// beside the ctr pass's two (VALU-bound ctr waves and LDS-bound GHASH waves
+// share the CU); `st` waits for bs.aux before the batch completes.
+static int launch_gcm_bs(const GcmParams &p, int encrypt, int two_pass, int grid, hipStream_t st,
+                         const GcmBsLaunch &bs) {
+  constexpr int WG = 1024, S = kGcmLanesPerRec;
+  GcmParams pc = p;
+  pc.queue = p.queue + 4;
+  const int cgrid = 2 * grid;                                 // two ctr workgroups per CU
+  if (encrypt) {
+    hipLaunchKernelGGL((gcm_bsctr_kernel<1, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 1, WG, S>), dim3(grid), dim3(WG), 0, st, p);
+  } else if (two_pass) {
+    hipLaunchKernelGGL((gcm_split_kernel<0, 3, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_bsctr_kernel<2, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
+  } else if (bs.mode >= 2 && bs.aux != nullptr) {
+    hipStream_t aux = bs.mode == 3 ? st : reinterpret_cast<hipStream_t>(bs.aux);   // 3: debug, one stream
+    hipEvent_t fork = reinterpret_cast<hipEvent_t>(bs.ev_fork), join = reinterpret_cast<hipEvent_t>(bs.ev_join);
+    if (hipEventRecord(fork, st) != hipSuccess || hipStreamWaitEvent(aux, fork, 0) != hipSuccess) return -1;
+    hipLaunchKernelGGL((gcm_bsctr_kernel<0, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
+    hipLaunchKernelGGL((gcm_split_kernel<0, 4, 256, 2>), dim3(grid), dim3(256), 0, aux, p);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 0, 256, S>), dim3(grid), dim3(256), 0, aux, p);
+    if (hipEventRecord(join, aux) != hipSuccess || hipStreamWaitEvent(st, join, 0) != hipSuccess) return -1;
+  } else {
+    hipLaunchKernelGGL((gcm_bsctr_kernel<0, true>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
+    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream,
+               const GcmBsLaunch *bs) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   constexpr int W = kGcmLanesSmall;
@@ -1522,6 +1831,7 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
   if (!small) p.chunk = (GCM_WG / 64) * (64 / kGcmLanesPerRec);   // experiment: one pass per chunk
 #endif
   if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + p.chunk - 1) / p.chunk)));
+  if (!small && p.ej0 != nullptr && bs != nullptr && bs->mode) return launch_gcm_bs(p, encrypt, two_pass, grid, st, *bs);
   if (!small && p.ej0 != nullptr) return launch_gcm_split(p, encrypt, two_pass, grid, st);
   if (burst) {
     if (p.xin != nullptr && p.chunks != nullptr) return -1;   // self-staging: implicit chunks only

@@ -161,6 +161,12 @@ struct espgpu_ctx {
   // kernel, 1 = the ctr pass + tag pass (esp_gcm.hip gcm_split_kernel), which
   // keep E_K(J0) per record in d_ej0
   int gcm_split = 0;
+  // Bitsliced ctr pass for large batches (set_tuning "gcm_bs", esp_gcm.hip
+  // gcm_bsctr_kernel): 0 = off, 1 = ctr pass then tag pass, 2 = out-of-place
+  // decrypt with the tag pass concurrently on s_aux (fork/join events)
+  int gcm_bs = 0;
+  hipStream_t s_aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint4 *d_ej0 = nullptr;
   uint32_t ej0_cap = 0;
   // planner workspace
@@ -402,7 +408,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   // the burst kernel (small batches of <= gcm_burst records, out of place or
   // encrypt; launch_gcm picks the kernel from it)
   const bool gsmall = c->gcm_lanes ? c->gcm_lanes == kGcmLanesSmall : n < kGcmSmallBatch;
-  if ((kinds & 1) && ((c->gcm_split && !gsmall) || (gsmall && !two_pass && n <= c->gcm_burst))) {
+  if ((kinds & 1) && (((c->gcm_split || c->gcm_bs) && !gsmall) || (gsmall && !two_pass && n <= c->gcm_burst))) {
     if (n > c->ej0_cap) {
       hipFree(c->d_ej0);
       c->d_ej0 = nullptr;
@@ -412,7 +418,8 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     }
     p.ej0 = c->d_ej0;
   }
-  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, c->gcm_lanes, st))
+  const GcmBsLaunch bs{c->gcm_bs, c->s_aux, c->ev_fork, c->ev_join};
+  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, c->gcm_lanes, st, &bs))
     return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if ((kinds & 2) && c->n_eta > 0) {
     EtaParams q{};
@@ -478,7 +485,8 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     if (hipSetDevice(cfg.device) != hipSuccess) { rc = fail(c, ESPGPU_ENODEV, "hipSetDevice failed"); break; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_aux, hipStreamNonBlocking) != hipSuccess) {
       rc = fail(c, ESPGPU_EIO, "stream");
       break;
     }
@@ -489,18 +497,20 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     hipEventCreate(&c->ev0);
     hipEventCreate(&c->ev1);
     hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     c->ready.reserve((size_t)cfg.batch_records * cfg.nbatches + 1024);
     if (hipMalloc(&c->d_sas, (size_t)cfg.max_sessions * sizeof(DevSA)) != hipSuccess ||
         hipMalloc(&c->d_gtab, (size_t)cfg.max_sessions * kGhTableBytes) != hipSuccess ||
         hipMalloc(&c->d_tpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_dpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_isbox, 256) != hipSuccess ||
-        hipMalloc(&c->d_queue, 16) != hipSuccess) {
+        hipMalloc(&c->d_queue, 32) != hipSuccess) {
       rc = fail(c, ESPGPU_ENOMEM, "device SA table allocation failed");
       break;
     }
     hipMemset(c->d_sas, 0, (size_t)cfg.max_sessions * sizeof(DevSA));
-    hipMemset(c->d_queue, 0, 16);
+    hipMemset(c->d_queue, 0, 32);
     const hc::Tables &t = hc::tables();
     uint2 tp[256], dp[256];
     for (int x = 0; x < 256; ++x) {
@@ -525,7 +535,7 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
 
 void espgpu_fini(espgpu_ctx *c) {
   if (!c) return;
-  for (hipStream_t st : {c->s_in, c->stream, c->s_out})
+  for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux})
     if (st) hipStreamSynchronize(st);
   for (auto &s : c->slots) free_slot(s);
   for (const HostRegion &r : c->regions)
@@ -542,7 +552,9 @@ void espgpu_fini(espgpu_ctx *c) {
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->ev_last) hipEventDestroy(c->ev_last);
-  for (hipStream_t st : {c->s_in, c->stream, c->s_out})
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  if (c->ev_join) hipEventDestroy(c->ev_join);
+  for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux})
     if (st) hipStreamDestroy(st);
   delete c;
 }
@@ -639,6 +651,9 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     for (int i = 0; i < 4; ++i) sa.rk[i] = rk[i];
     for (int i = 4; i < 4 * nr; ++i) sa.rk[i] = ror16(rk[i]);
     for (int i = 0; i < 4; ++i) sa.rk[4 * nr + i] = bswap(rk[4 * nr + i]);
+    // bitsliced ctr pass (aes_bs.h): K0, then K_r ^ 0x63..63 (the S-box
+    // circuit's affine constant), little-endian words
+    for (int i = 0; i < 4 * (nr + 1); ++i) sa.dk[i] = bswap(rk[i]) ^ (i >= 4 ? 0x63636363u : 0u);
     uint8_t zero[16] = {0}, h[16];
     hc::aes_encrypt_block(rk, nr, zero, h);       // H = E_K(0^128), gmac.c:56-60
     std::vector<uint8_t> tabs(kGhTableBytes);
@@ -1330,6 +1345,11 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!strcmp(key, "gcm_split")) {
     if (value != 0 && value != 1) return ESPGPU_EINVAL;
     c->gcm_split = value;
+    return 0;
+  }
+  if (!strcmp(key, "gcm_bs")) {
+    if (value < 0 || value > 3) return ESPGPU_EINVAL;
+    c->gcm_bs = value;
     return 0;
   }
   if (!strcmp(key, "gcm_lanes")) {

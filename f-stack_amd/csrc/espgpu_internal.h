@@ -12,7 +12,9 @@ namespace espgpu {
 // GCM: rk[] is the AES encryption schedule in "kernel form" for the pair-table
 //   round (esp_gcm.hip): rk[0..3] raw, rk[4r..4r+3] = ror16(rk) for the
 //   middle rounds, rk[4nr..] byte-swapped (the last round emits little-endian
-//   words).  The GHASH tables live in a separate array.
+//   words); dk[] = the schedule for the bitsliced ctr pass (aes_bs.h): K0 and
+//   K_r ^ 0x63636363 (r >= 1) as little-endian words.  The GHASH tables live
+//   in a separate array.
 // ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
 //   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
 //   = SHA-1 chaining state after one block of key^0x36 / key^0x5c
@@ -143,7 +145,15 @@ constexpr uint32_t kXferPiece = 4096;
 // Launchers (defined in the .hip files, called by espgpu.cpp).
 // lanes: 0 = by batch size (kGcmLanesSmall below kGcmSmallBatch records,
 // else kGcmLanesPerRec), or force 4 / 8 (set_tuning "gcm_lanes", tests)
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int lanes, void *stream);
+// The bitsliced ctr pass for large batches (set_tuning "gcm_bs"): mode 0 off,
+// 1 ctr pass then tag pass on the stream, 2 out-of-place decrypt with the tag
+// pass on `aux` concurrently (ev_fork / ev_join order it against the stream).
+struct GcmBsLaunch {
+  int mode;
+  void *aux, *ev_fork, *ev_join;
+};
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int lanes, void *stream,
+               const GcmBsLaunch *bs = nullptr);
 int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
 int set_eta_opts(uint32_t opts);
 // kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones

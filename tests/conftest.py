@@ -35,22 +35,26 @@ def pytest_configure(config):
     _make(["-C", "f-stack_amd", "-j8"])
 
 
-@pytest.fixture(params=[(4, 0, 0), (8, 0, 0), (4, 1, 0), (8, 0, 1 << 30)],
-                ids=["lanes4", "lanes8", "split", "burst"])
+@pytest.fixture(params=[(4, 0, 0, 0), (8, 0, 0, 0), (4, 1, 0, 0), (8, 0, 1 << 30, 0), (4, 0, 0, 1), (4, 0, 0, 2)],
+                ids=["lanes4", "lanes8", "split", "burst", "bs", "bsconc"])
 def gcm_lanes(request, drv):
     """Run a GCM test through every GCM kernel design whatever its batch
     size: the fused kernel with 4 lanes per record (throughput) and with 8
     (small batches, half the serial steps), the split design (a CTR pass
-    then a GHASH / tag pass) and the burst kernel (both passes in one launch;
-    decrypt in place keeps the fused kernel); set_tuning "gcm_lanes" /
-    "gcm_split" / "gcm_burst", reset afterwards."""
-    lanes, split, burst = request.param
+    then a GHASH / tag pass), the burst kernel (both passes in one launch;
+    decrypt in place keeps the fused kernel) and the bitsliced ctr pass with
+    the tag pass after it (bs) or, decrypting out of place, beside it on a
+    second stream (bsconc); set_tuning "gcm_lanes" / "gcm_split" /
+    "gcm_burst" / "gcm_bs", reset afterwards."""
+    lanes, split, burst, bs = request.param
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", lanes) == 0
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", split) == 0
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_burst", burst) == 0
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", bs) == 0
     try:
         yield lanes
     finally:
         drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", 0)
         drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0)
         drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_burst", 4096)
+        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", 0)

@@ -27,8 +27,10 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--opts", type=int, nargs="*", default=[0],
                     help="measurement knobs (libespgpu built with make KNOBS=1): 1 no loads/stores, "
-                         "2 no GHASH, 4 no AES rounds 3+")
+                         "2 no GHASH, 4 no AES rounds 3+; bitsliced ctr pass (gcm_bs): 128 no rounds, "
+                         "256 no memory side, 512 no transposes")
     ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--tuning", action="append", default=[], help="espgpu_set_tuning key=value (e.g. gcm_bs=1)")
     args = ap.parse_args()
     import torch
     from espgpu.batch import decrypt_batch
@@ -50,6 +52,9 @@ def main():
     stream = torch.cuda.Stream()
     algo = n * (rl + 16) + n * (rl - 32) + n
     drv.lib.espgpu_set_tuning(drv.ctx, b"grid", args.grid)
+    for kv in args.tuning:
+        k, v = kv.split("=")
+        assert drv.lib.espgpu_set_tuning(drv.ctx, k.encode(), int(v)) == 0, kv
     for s in args.opts:
         if s:
             assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_opts", s) == 0, "knobs need a KNOBS=1 build"
