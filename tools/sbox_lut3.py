@@ -4,7 +4,8 @@
 # prints the C body pasted into f-stack_amd/csrc/aes_bs.h sbox().
 # Greedy LUT3 packing of the Boyar-Peralta S-box (from t2 on; y*, X7 are inputs)
 import re
-src=open('__import__('os').path.join(__import__('os').path.dirname(__file__), 'sbox_circuit.py')').read()
+import os
+src=open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'sbox_circuit.py')).read()
 circ=src.split('CIRCUIT = """')[1].split('"""')[0].strip().splitlines()
 gates=[]
 for l in circ:
