@@ -1789,8 +1789,8 @@ static int launch_gcm_bs(const GcmParams &p, int encrypt, int two_pass, int grid
     hipLaunchKernelGGL((gcm_split_kernel<0, 3, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
     hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
     hipLaunchKernelGGL((gcm_bsctr_kernel<2, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
-  } else if (bs.mode >= 2 && bs.aux != nullptr) {
-    hipStream_t aux = bs.mode == 3 ? st : reinterpret_cast<hipStream_t>(bs.aux);   // 3: debug, one stream
+  } else if (bs.mode == 2 && bs.aux != nullptr) {
+    hipStream_t aux = reinterpret_cast<hipStream_t>(bs.aux);
     hipEvent_t fork = reinterpret_cast<hipEvent_t>(bs.ev_fork), join = reinterpret_cast<hipEvent_t>(bs.ev_join);
     if (hipEventRecord(fork, st) != hipSuccess || hipStreamWaitEvent(aux, fork, 0) != hipSuccess) return -1;
     hipLaunchKernelGGL((gcm_bsctr_kernel<0, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);

@@ -1348,7 +1348,7 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
     return 0;
   }
   if (!strcmp(key, "gcm_bs")) {
-    if (value < 0 || value > 3) return ESPGPU_EINVAL;
+    if (value < 0 || value > 2) return ESPGPU_EINVAL;
     c->gcm_bs = value;
     return 0;
   }

@@ -331,6 +331,11 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *   "gcm_split" GCM batches of >= 32768 records (or any size with gcm_lanes
  *               4): 1 = a CTR pass (16 lanes per record) then a GHASH / tag
  *               pass, 0 = the fused kernel;
+ *   "gcm_bs"    GCM batches of >= 32768 records (or gcm_lanes 4): 1 = the
+ *               bitsliced CTR pass (AES on the VALU, 32 counter blocks per
+ *               lane) then the GHASH / tag pass; 2 = the same, out-of-place
+ *               decrypt with the tag pass on a second stream; 0 (default) =
+ *               by gcm_split; others EINVAL;
  *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
  *               decrypt (MODE 3) out of place, 1 one fused pass per record
  *               (MODE 0), 0 separate verify / decrypt kernels; others EINVAL;

@@ -668,3 +668,12 @@ def test_grouped_batch_sizes_across_the_small_batch_path(drv, n):
     assert (arena.cpu().numpy() == ct).all()
     for s in sids:
         drv.freesession(s)
+
+
+def test_gcm_bs_knob_range(drv):
+    """set_tuning "gcm_bs" takes 0, 1, 2 (the bitsliced CTR pass) and refuses
+    anything else with EINVAL, leaving the setting unchanged."""
+    for v in (-1, 3, 9):
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 22
+    for v in (2, 1, 0):
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 0
