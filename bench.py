@@ -294,14 +294,15 @@ def main():
 
 def launched_kernel(cfg, inplace):
     """Source name of the kernel the timed loop launches (the one the roofline
-    prices): gcm_kernel<MODE, 1024, S> with MODE 0 = out-of-place decrypt, 2 =
-    in-place verify-first, S = 4 lanes per record (every bench config has
-    >= 32K records: the small-batch S = 8 kernel is not launched);
+    prices): gcm_kernel<MODE, 1024, S, STAGE> with MODE 0 = out-of-place
+    decrypt, 2 = in-place verify-first, S = 4 lanes per record (every bench
+    config has >= 32K records: the small-batch S = 8 kernel is not launched),
+    STAGE false (device-resident records);
     eta_kernel<3 (out of place) / 2 (in place), 768, -2> for CBC + HMAC-SHA1
     (verify pass, then the block-parallel decrypt of the verified records; -2 =
     the launch for SHA-1 / SHA2-256 sessions, esp_cbc.hip CK_NARROW)."""
     if cfg["alg"] == "gcm":
-        return "gcm_kernel<%d, 1024, 4>" % (2 if inplace else 0)
+        return "gcm_kernel<%d, 1024, 4, false>" % (2 if inplace else 0)
     return "eta_kernel<2, 768, -2>" if inplace else "eta_kernel<3, 768, -2>"   # verify-first two-pass
 
 
@@ -390,7 +391,7 @@ def encrypt_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, world, 
         b = torch.tensor([float(pkt_bytes)], dtype=torch.float64, device=arena.device)
         dist.all_reduce(b, op=dist.ReduceOp.SUM)
         ms, pkt_bytes = float(t.item()), float(b.item())
-    kernel = "gcm_kernel<1, 1024, 4>" if cfg["alg"] == "gcm" else "eta_kernel<1, 768, -1>"
+    kernel = "gcm_kernel<1, 1024, 4, false>" if cfg["alg"] == "gcm" else "eta_kernel<1, 768, -1>"
     return {"value": round(pkt_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "kernel_ms": round(ms, 4),
             "status_ok": ok, "timing": "median of %d launches, HIP events around the encrypt only" % reps,
             "kernel": kernel + " (in place, ICV written)"}
