@@ -17,7 +17,9 @@
 // every byte: the caller passes K'_r = K_r ^ 0x63..63 for r >= 1
 // (rijndaelEncrypt's round structure, rijndael-alg-fst.c:863-1042).
 #pragma once
+#ifndef ESPGPU_HOST_SHIM   // tools/aes_bs_selftest.cpp builds this header for the CPU
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 namespace espgpu {
@@ -183,6 +185,38 @@ __device__ __forceinline__ void round(uint32_t (&st)[128], const uint32_t *kprev
   }
 #pragma unroll
   for (int i = 0; i < 128; ++i) st[i] = o[i];
+}
+
+// 32x32 bit transpose: afterwards bit i of a[s] = bit s of the old a[i]
+// (swapmove ladder; the 16- and 8-bit stages are byte moves).  Applied to the
+// 32 registers of state bytes 4g..4g+3 it turns them into word g (memory
+// order) of each of the 32 blocks.
+__device__ __forceinline__ void transpose32(uint32_t *a) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t x = a[k], y = a[k + 16];
+    a[k] = __builtin_amdgcn_perm(y, x, 0x05040100u);
+    a[k + 16] = __builtin_amdgcn_perm(y, x, 0x07060302u);
+  }
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if (k & 8) continue;
+    const uint32_t x = a[k], y = a[k + 8];
+    a[k] = __builtin_amdgcn_perm(y, x, 0x06020400u);
+    a[k + 8] = __builtin_amdgcn_perm(y, x, 0x07030501u);
+  }
+  constexpr uint32_t M[3] = {0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int j = 4 >> q;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      if (k & j) continue;
+      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & M[q];
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
 }
 
 }  // namespace bs

@@ -1494,36 +1494,6 @@ __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
 constexpr int kBsWG = 256;                 // one wave per SIMD; two workgroups per CU
 constexpr uint32_t kBsQuarter = 8 * 64 * 16;   // LDS bytes of one quarter buffer (8 blocks x 64 windows)
 
-// 32x32 bit transpose: afterwards bit i of a[s] = bit s of the old a[i]
-// (swapmove ladder; the 16- and 8-bit stages are byte moves)
-__device__ __forceinline__ void bs_transpose32(uint32_t *a) {
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t x = a[k], y = a[k + 16];
-    a[k] = perm(y, x, 0x05040100u);
-    a[k + 16] = perm(y, x, 0x07060302u);
-  }
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    if (k & 8) continue;
-    const uint32_t x = a[k], y = a[k + 8];
-    a[k] = perm(y, x, 0x06020400u);
-    a[k + 8] = perm(y, x, 0x07030501u);
-  }
-  constexpr uint32_t M[3] = {0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int j = 4 >> q;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      if (k & j) continue;
-      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & M[q];
-      a[k + j] ^= t;
-      a[k] ^= t << j;
-    }
-  }
-}
-
 template <int DIR, bool SEQ>
 __global__ __launch_bounds__(kBsWG) __attribute__((amdgpu_waves_per_eu(2), amdgpu_num_vgpr(GCM_BS_VGPRS)))
 void gcm_bsctr_kernel(GcmParams p) {
@@ -1661,7 +1631,7 @@ void gcm_bsctr_kernel(GcmParams p) {
       // keystream blocks: word g of slice s -> st[32g + s], last round key added
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        if (!(gopts() & 512)) bs_transpose32(&st[32 * g]);
+        if (!(gopts() & 512)) bs::transpose32(&st[32 * g]);
         const uint32_t kl = K[4 * nr + g];
 #pragma unroll
         for (int s = 0; s < 32; ++s) st[32 * g + s] ^= kl;

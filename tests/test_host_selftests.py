@@ -28,3 +28,19 @@ def test_ghash_table_layout_selftest(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]
     assert "OK" in r.stdout
+
+
+def test_bitsliced_aes_selftest(tmp_path):
+    """The bitsliced AES of the gcm_bs ctr pass (aes_bs.h: the LUT3-packed
+    S-box circuit, key folding, affine constant in the round keys, 32x32
+    transposes), built for the CPU with its two gfx950 builtins emulated,
+    against host_crypto's table AES for AES-128/192/256 counter windows
+    (tools/aes_bs_selftest.cpp)."""
+    exe = tmp_path / "aes_bs_selftest"
+    csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
+                    os.path.join(ROOT, "tools", "aes_bs_selftest.cpp"),
+                    os.path.join(csrc, "host_crypto.cpp")], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert r.stdout.startswith("OK")
