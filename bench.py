@@ -285,6 +285,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(pristine if args.inplace else arena, d, sids, keys, args,
                                               n, cfg)
+        try:
+            result["cpu_openssl"] = cpu_openssl(pristine if args.inplace else arena, d, sids, keys, args,
+                                                n, cfg)
+        except Exception as e:                   # informational only (needs tools/libossl_esp.so)
+            log("cpu_openssl skipped: %s" % e)
     if rank == 0:
         print(json.dumps(result), flush=True)
     drv.close()
@@ -547,6 +552,47 @@ def cpu_baseline(arena, d, sids, keys, args, n, cfg):
                       % (m, args.config, per_thread, threads,
                          "swcr_gcm" if cfg["alg"] == "gcm" else "swcr_eta", len(runs),
                          sum(runs) * threads)}
+
+
+def cpu_openssl(arena, d, sids, keys, args, n, cfg):
+    """OpenSSL 3 EVP (AES-NI / VAES / PCLMULQDQ) on the same records and
+    threads as cpu_baseline: NOT the reference path (F-Stack's kernel crypto
+    is cryptosoft's table code), a comparison point only."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import ossl_esp
+    import ssl
+    if not ossl_esp.available():
+        raise RuntimeError("tools/libossl_esp.so not built")
+    share, _, _ = cpu_share()
+    threads = args.cpu_threads or share
+    m = min(n, 65536 * threads)
+    sample = d[:m].copy()
+    lo = int(sample["off4"][0]) * 4
+    hi = int(sample["off4"][-1]) * 4 + int(sample["len"][-1])
+    host = arena[lo:hi + 16].cpu().numpy().copy()
+    sample["off4"] -= lo // 4
+    sa_idx = np.searchsorted(np.array(sids), sample["sa"])
+    if cfg["alg"] == "gcm":
+        kw = dict(alg="gcm", ckeys=[k[:-4] for k in keys], salts=[k[-4:] for k in keys], mlen=16)
+    else:
+        kw = dict(alg="cbc_sha1", ckeys=[k[0] for k in keys], akeys=[k[1] for k in keys], mlen=12)
+    runs = []
+    for _ in range(max(1, args.cpu_runs)):
+        t, st = ossl_esp.batch_decrypt(arena=host.copy(), off4=sample["off4"], lens=sample["len"],
+                                       sa_idx=sa_idx, nthreads=threads, **kw)
+        assert (st == 0).all(), "OpenSSL rejected GPU-encrypted records"
+        runs.append(t)
+    t1, st1 = ossl_esp.batch_decrypt(arena=host.copy(), off4=sample["off4"][:16384], lens=sample["len"][:16384],
+                                     sa_idx=sa_idx[:16384], nthreads=1, **kw)
+    assert (st1 == 0).all()
+    tN = sorted(runs)[len(runs) // 2]
+    pkt_bytes = (sample["len"].astype(np.int64) + cfg["skip"])
+    return {"value": round(float(pkt_bytes.sum()) / tN / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "openssl, not the reference path", "library": ssl.OPENSSL_VERSION,
+            "median_of": len(runs), "runs_s": [round(t, 4) for t in runs],
+            "one_core_GBps": round(float(pkt_bytes[:16384].sum()) / t1 / 1e9, 3),
+            "sample": "the cpu_baseline records (%d) on %d threads, EVP %s in place, verify + decrypt"
+                      % (m, threads, "AES-GCM" if cfg["alg"] == "gcm" else "AES-CBC + HMAC-SHA1")}
 
 
 if __name__ == "__main__":

@@ -70,6 +70,9 @@
 #ifndef GCM_SPLIT_WPE
 #define GCM_SPLIT_WPE 4
 #endif
+#ifndef GCM_ALIGNED
+#define GCM_ALIGNED 1
+#endif
 
 namespace espgpu {
 
@@ -620,7 +623,96 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   constexpr bool PF = GCM_PREFETCH && S == kGcmLanesSmall;
   uint4 pCa = make_uint4(0, 0, 0, 0), pCb = make_uint4(0, 0, 0, 0);
   int pf_m = -1;                                            // step held in pCa / pCb
-  int m = 0;
+  // Aligned schedule (MODE 0 / 1, S = 4, every record of the wave with pad =
+  // S - 1, i.e. nct + 1 a multiple of S, as 1500-byte packets are): the AES
+  // work is decoupled from the GHASH positions.  GHASH is unchanged (block i
+  // = S*g + l - pad at step g), but the counter blocks are dealt out densely,
+  // lane l of AES step a taking slot j = S*a + l (CT block j, or J0 in slot
+  // nct), so a record runs nct + 1 = S*Ma block encryptions instead of S*M =
+  // S*(Ma + 1): the front padding and the length block get none.  With pad =
+  // S - 1 GHASH step a + 1 of lane l hashes exactly slot j of AES step a, so
+  // the ciphertext a lane loaded (or, encrypting, produced) is hashed one step
+  // later from its own registers.
+  const bool aligned = GCM_ALIGNED && MODE != 2 && S == kGcmLanesPerRec && __all(!valid || pad == S - 1);
+  int m = aligned ? Mw : 0;
+  if (aligned) {
+    const int Ma = valid ? M - 1 : 0;
+    int Maw = Ma;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Maw = max(Maw, __shfl_xor(Maw, o));
+    // GHASH block of AES slot j: the (masked) ciphertext, the length block in
+    // slot nct; C = this slot's ciphertext, ks its keystream; also stores
+    // the slot's output and notes E_K(J0) / the trailer word
+    auto slot_out = [&](int j, uint4 C, uint4 ks) -> uint4 {
+      if (!valid || j > nct) return make_uint4(0, 0, 0, 0);
+      if (j == nct) {
+        EJ0 = ks;
+        return make_uint4(0, bswap32(sep ? 96u : 64u), 0, bswap32((uint32_t)ct_len * 8));
+      }
+      const int rem = ct_len - 16 * j;
+      const uint4 o = xor4(C, ks);
+      if (!(gopts() & 9)) st_partial(orec + 16 + 16 * j, o, rem);
+      if (MODE == 0) note_trailer(j + 1, o, rem);
+      return mask_block(MODE == 1 ? o : C, rem);
+    };
+    uint4 prev = (valid && l == S - 1) ? (sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0))
+                                       : make_uint4(0, 0, 0, 0);      // GHASH step 0: AAD / padding
+    for (int a = 0; a < Maw; a += 2) {
+      const int ja = S * a + l, jb = ja + S;
+      const uint32_t ca = ja < nct ? (uint32_t)ja + 2 : 1u, cb = jb < nct ? (uint32_t)jb + 2 : 1u;
+      const bool two = a + 1 < Maw;                                  // wave-uniform
+      if (two && a > 0 && __all(!valid || 16 * (jb + 1) <= ct_len)) {
+        // interior: both slots full ciphertext blocks for every record
+        if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
+        if (__all((int)(cb >> 8) == cc.hi)) {
+          uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+          if (valid && !(gopts() & 17)) {
+            Ca = ld16(rec + 16 + 16 * ja);
+            Cb = ld16(rec + 16 + 16 * jb);
+          }
+          uint4 ka, kb;
+          aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+          const uint4 Oa = xor4(Ca, ka), Ob = xor4(Cb, kb);
+          if (valid && !(gopts() & 9)) {
+            st16(orec + 16 + 16 * ja, Oa);
+            st16(orec + 16 + 16 * jb, Ob);
+          }
+          const uint4 Ba = MODE == 1 ? Oa : Ca;
+          if (gopts() & 2)
+            Y = xor4(xor4(Y, prev), Ba);
+          else
+            Y = xor4(gf_mul8(xor4(gf_mul8(Y, lds, gl), prev), lds, gl), Ba);
+          prev = MODE == 1 ? Ob : Cb;
+          continue;
+        }
+      }
+      // general pair (or single last AES step): per-lane slot kinds
+      uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+      if (valid && ja < nct && !(gopts() & 17)) Ca = ld16(rec + 16 + 16 * ja);
+      if (two && valid && jb < nct && !(gopts() & 17)) Cb = ld16(rec + 16 + 16 * jb);
+      // (the edge steps of a record: one block at a time, so the general path
+      // holds one keystream block and inlines no second pair round)
+      if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
+      const uint4 Ba = a < Ma ? slot_out(ja, Ca, aes_ctr(cc, ca, rk3, nr, rk, lds, slot)) : make_uint4(0, 0, 0, 0);
+      uint4 Bb = make_uint4(0, 0, 0, 0);
+      if (two) {
+        if ((int)(cb >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(cb >> 8), rk, lds, slot);
+        const uint4 kb = aes_ctr(cc, cb, rk3, nr, rk, lds, slot);
+        if (a + 1 < Ma) Bb = slot_out(jb, Cb, kb);
+      }
+      // GHASH steps a (block prev) and a + 1 (block Ba), each only if <= Ma
+      const uint4 Ym = a == 0 ? prev : xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), prev);
+      if (valid && a <= Ma) Y = Ym;
+      const uint4 Yn = xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), Ba);
+      if (valid && a + 1 <= Ma) Y = Yn;
+      prev = Bb;
+    }
+    if ((Maw & 1) == 0 && Maw > 0) {
+      // GHASH step Maw (the last block of the records with Ma == Maw)
+      const uint4 Yn = xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), prev);
+      if (valid && Ma == Maw) Y = Yn;
+    }
+  }
   while (m < Mw) {
     const int i = S * m + l - pad;
     if (m + 1 < Mw && (MODE != 2 || m > 0)) {
