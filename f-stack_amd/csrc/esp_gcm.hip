@@ -858,22 +858,40 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     }
   }
   if (MODE == 2) {
-    // pass 2: CTR decrypt in place, only for authenticated records
+    // pass 2: CTR decrypt in place, only for authenticated records.  No GHASH
+    // here, so the CT blocks are dealt densely (lane l of step a: block
+    // S*a + l, no padding or length-block slots), two blocks per lane per
+    // step, each step's loads issued before its rounds.
     const int run = valid && ok;
-    int Mr = run ? M : 0;
+    int Mr = run ? (nct + S - 1) / S : 0;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
-    for (int m = 0; m < Mr; ++m) {
-      const int i = S * m + l - pad;
-      const uint32_t ctr = i >= 0 ? (uint32_t)(i + 1) : 1u;
-      if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
-      const uint4 ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
-      if (run && i >= 1 && i <= nct) {
-        const int c = i - 1;
-        const uint4 C = ld16(rec + 16 + 16 * c);
+    auto put = [&](int c, uint4 C, uint4 ks) {
+      if (run && c < nct) {
         const uint4 pt = xor4(C, ks);
         st_partial(rec + 16 + 16 * c, pt, ct_len - 16 * c);
-        note_trailer(i, pt, ct_len - 16 * c);
+        note_trailer(c + 1, pt, ct_len - 16 * c);
+      }
+    };
+    for (int a = 0; a < Mr; a += 2) {
+      const int ca = S * a + l, cb = ca + S;
+      const bool two = a + 1 < Mr;                                   // wave-uniform
+      uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
+      if (run && ca < nct) Ca = ld16(rec + 16 + 16 * ca);
+      if (two && run && cb < nct) Cb = ld16(rec + 16 + 16 * cb);
+      const uint32_t ta = (uint32_t)ca + 2, tb = (uint32_t)cb + 2;
+      if ((int)(ta >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ta >> 8), rk, lds, slot);
+      if (two && __all((int)(tb >> 8) == cc.hi)) {
+        uint4 ka, kb;
+        aes_ctr2(cc, ta, tb, rk3, nr, rk, lds, slot, ka, kb);
+        put(ca, Ca, ka);
+        put(cb, Cb, kb);
+      } else {
+        put(ca, Ca, aes_ctr(cc, ta, rk3, nr, rk, lds, slot));
+        if (two) {
+          if ((int)(tb >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(tb >> 8), rk, lds, slot);
+          put(cb, Cb, aes_ctr(cc, tb, rk3, nr, rk, lds, slot));
+        }
       }
     }
   }

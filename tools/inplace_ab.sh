@@ -1,0 +1,13 @@
+#!/bin/bash
+# Same-box A/B of engine builds on the in-place (verify-first) decrypt of one
+# configuration: alternating runs, kernel ms of each.
+#   bash tools/inplace_ab.sh <cfg> <lib1> <lib2> ... (run on the GPU box)
+set -e
+CFG=$1; shift
+B="python bench.py --config $CFG --inplace --steps 20 --warmup 10 --no-cpu --no-e2e --no-encrypt-leg"
+for k in 1 2 3; do
+  for L in "$@"; do
+    echo -n "$L "
+    ESPGPU_LIB=$L timeout -k 10 120 $B 2>/dev/null | python -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['ms_per_step'], d['roofline']['kernel_ms'])"
+  done
+done
