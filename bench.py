@@ -576,23 +576,29 @@ def cpu_openssl(arena, d, sids, keys, args, n, cfg):
         kw = dict(alg="gcm", ckeys=[k[:-4] for k in keys], salts=[k[-4:] for k in keys], mlen=16)
     else:
         kw = dict(alg="cbc_sha1", ckeys=[k[0] for k in keys], akeys=[k[1] for k in keys], mlen=12)
+    # out of place (the headline's mode), the sample REPS times over per run,
+    # so a run lasts ~1 s and the cgroup quota's 100-ms periods average out
+    REPS = 8
+    out = np.empty_like(host)
     runs = []
     for _ in range(max(1, args.cpu_runs)):
-        t, st = ossl_esp.batch_decrypt(arena=host.copy(), off4=sample["off4"], lens=sample["len"],
-                                       sa_idx=sa_idx, nthreads=threads, **kw)
+        t, st = ossl_esp.batch_decrypt(arena=host, off4=sample["off4"], lens=sample["len"], sa_idx=sa_idx,
+                                       nthreads=threads, out=out, reps=REPS, **kw)
         assert (st == 0).all(), "OpenSSL rejected GPU-encrypted records"
-        runs.append(t)
-    t1, st1 = ossl_esp.batch_decrypt(arena=host.copy(), off4=sample["off4"][:16384], lens=sample["len"][:16384],
-                                     sa_idx=sa_idx[:16384], nthreads=1, **kw)
+        runs.append(t / REPS)
+    t1, st1 = ossl_esp.batch_decrypt(arena=host, off4=sample["off4"][:16384], lens=sample["len"][:16384],
+                                     sa_idx=sa_idx[:16384], nthreads=1, out=out, reps=REPS, **kw)
     assert (st1 == 0).all()
+    t1 /= REPS
     tN = sorted(runs)[len(runs) // 2]
     pkt_bytes = (sample["len"].astype(np.int64) + cfg["skip"])
     return {"value": round(float(pkt_bytes.sum()) / tN / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "openssl, not the reference path", "library": ssl.OPENSSL_VERSION,
             "median_of": len(runs), "runs_s": [round(t, 4) for t in runs],
             "one_core_GBps": round(float(pkt_bytes[:16384].sum()) / t1 / 1e9, 3),
-            "sample": "the cpu_baseline records (%d) on %d threads, EVP %s in place, verify + decrypt"
-                      % (m, threads, "AES-GCM" if cfg["alg"] == "gcm" else "AES-CBC + HMAC-SHA1")}
+            "sample": "the cpu_baseline records (%d) on %d threads, EVP %s out of place, verify + decrypt, "
+                      "%d passes per run (seconds per pass)"
+                      % (m, threads, "AES-GCM" if cfg["alg"] == "gcm" else "AES-CBC + HMAC-SHA1", REPS)}
 
 
 if __name__ == "__main__":

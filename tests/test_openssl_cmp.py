@@ -60,3 +60,23 @@ def test_openssl_cbc_sha1_matches_oracle():
     assert t > 0
     assert (st == st_ref).all() and (st[3::9] == 74).all()
     assert (work == ref).all()       # verified records decrypted in place, failed ones untouched
+
+
+def test_openssl_out_of_place_repeated():
+    """The bench's mode: out of place, the sample several times over; the input
+    is never written and every pass yields the oracle's plaintext."""
+    rng = np.random.default_rng(5)
+    sas = [GcmSA(rng) for _ in range(2)]
+    n = 64
+    sa_idx = rng.integers(0, 2, n)
+    _, ct, descs, esn = build_records(rng, sas, sa_idx, np.full(n, 1448))
+    ref, st_ref = oracle_decrypt(sas, ct, descs, esn)
+    src = ct.copy()
+    out = np.zeros_like(ct)
+    t, st = ossl_esp.batch_decrypt("gcm", [s.key for s in sas], src, descs["off4"], descs["len"], descs["sa"],
+                                   salts=[s.salt for s in sas], nthreads=2, out=out, reps=3)
+    assert t > 0 and (st == 0).all() and (st_ref == 0).all()
+    assert (src == ct).all()
+    for i in range(n):
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        assert out[o + 16:o + L - 16].tobytes() == ref[o + 16:o + L - 16].tobytes()

@@ -2,7 +2,7 @@
  * OpenSSL EVP line, labelled not the reference path").
  *
  * Decrypts ESP records laid out as in the GPU batch ABI (arena + off4/len/sa
- * per record) in place on the host, with the same verify-first semantics as
+ * per record) on the host, in place or out of place, with the same verify-first semantics as
  * cryptosoft (swcr_gcm cryptosoft.c:465-645, swcr_eta :874-888): a record
  * whose ICV does not match is EBADMSG (74) and its payload is not used.
  * This is NOT the reference's algorithm: OpenSSL runs AES-NI/VAES and
@@ -30,7 +30,9 @@ enum { ST_OK = 0, ST_EINVAL = 22, ST_EBADMSG = 74 };
 struct job {
   int alg, nsa, cklen, aklen, mlen;
   const uint8_t *ckeys, *akeys, *salts;
-  uint8_t *arena;
+  const uint8_t *arena;
+  uint8_t *out;
+  int reps;
   const uint32_t *off4;
   const uint16_t *len, *sa_idx;
   uint8_t *status;
@@ -46,7 +48,8 @@ static const EVP_CIPHER *cbc_cipher(int klen) {
   return klen == 16 ? EVP_aes_128_cbc() : klen == 24 ? EVP_aes_192_cbc() : EVP_aes_256_cbc();
 }
 
-static uint8_t gcm_one(EVP_CIPHER_CTX *c, const uint8_t *salt, uint8_t *rec, int len, int mlen) {
+static uint8_t gcm_one(EVP_CIPHER_CTX *c, const uint8_t *salt, const uint8_t *rec, uint8_t *orec, int len,
+                       int mlen) {
   const int ct_len = len - 16 - mlen;
   if (ct_len <= 0 || (len & 3)) return ST_EINVAL;
   uint8_t nonce[12], tag[16];
@@ -56,12 +59,12 @@ static uint8_t gcm_one(EVP_CIPHER_CTX *c, const uint8_t *salt, uint8_t *rec, int
   memcpy(tag, rec + len - mlen, (size_t)mlen);
   if (EVP_DecryptInit_ex(c, NULL, NULL, NULL, nonce) != 1) return ST_EINVAL;
   if (EVP_DecryptUpdate(c, NULL, &ol, rec, 8) != 1) return ST_EINVAL;
-  if (EVP_DecryptUpdate(c, rec + 16, &ol, rec + 16, ct_len) != 1) return ST_EINVAL;
+  if (EVP_DecryptUpdate(c, orec + 16, &ol, rec + 16, ct_len) != 1) return ST_EINVAL;
   if (EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, mlen, tag) != 1) return ST_EINVAL;
-  return EVP_DecryptFinal_ex(c, rec + 16 + ol, &fl) > 0 ? ST_OK : ST_EBADMSG;
+  return EVP_DecryptFinal_ex(c, orec + 16 + ol, &fl) > 0 ? ST_OK : ST_EBADMSG;
 }
 
-static uint8_t eta_one(EVP_CIPHER_CTX *c, HMAC_CTX *h, uint8_t *rec, int len, int mlen) {
+static uint8_t eta_one(EVP_CIPHER_CTX *c, HMAC_CTX *h, const uint8_t *rec, uint8_t *orec, int len, int mlen) {
   const int plen = len - 24 - mlen;
   if (plen <= 0 || (plen & 15) || (len & 3)) return ST_EINVAL;
   uint8_t dg[EVP_MAX_MD_SIZE];
@@ -72,7 +75,7 @@ static uint8_t eta_one(EVP_CIPHER_CTX *c, HMAC_CTX *h, uint8_t *rec, int len, in
   if (memcmp(dg, rec + 24 + plen, (size_t)mlen) != 0) return ST_EBADMSG;   // verify first
   int ol = 0;
   if (EVP_DecryptInit_ex(c, NULL, NULL, NULL, rec + 8) != 1) return ST_EINVAL;
-  if (EVP_DecryptUpdate(c, rec + 24, &ol, rec + 24, plen) != 1) return ST_EINVAL;
+  if (EVP_DecryptUpdate(c, orec + 24, &ol, rec + 24, plen) != 1) return ST_EINVAL;
   return ST_OK;
 }
 
@@ -100,12 +103,13 @@ static void *worker(void *arg) {
   }
   if (!cc || !hh) j->err = 1;
   pthread_barrier_wait(j->bar);
-  if (!j->err) {
+  for (int r = 0; r < j->reps && !j->err; ++r) {
     for (uint32_t i = j->lo; i < j->hi; ++i) {
       const int s = j->sa_idx[i];
-      uint8_t *rec = j->arena + (size_t)j->off4[i] * 4;
-      j->status[i] = j->alg == 0 ? gcm_one(cc[s], j->salts + 4 * (size_t)s, rec, j->len[i], j->mlen)
-                                 : eta_one(cc[s], hh[s], rec, j->len[i], j->mlen);
+      const size_t o = (size_t)j->off4[i] * 4;
+      j->status[i] = j->alg == 0 ? gcm_one(cc[s], j->salts + 4 * (size_t)s, j->arena + o, j->out + o, j->len[i],
+                                           j->mlen)
+                                 : eta_one(cc[s], hh[s], j->arena + o, j->out + o, j->len[i], j->mlen);
     }
   }
   pthread_barrier_wait(j->bar);
@@ -124,14 +128,18 @@ static double now_s(void) {
   return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
-/* Decrypts n records in place with nthreads threads (contiguous record
- * ranges); fills status.  Returns the seconds between the two barriers that
- * bracket the record loop of every thread, or a negative value on error. */
+/* Decrypts n records with nthreads threads (contiguous record ranges), reps
+ * times over: plaintext to the same offsets of `out` (out == arena: in
+ * place; then reps must be 1); fills status.  Returns the seconds between the
+ * two barriers that bracket the record loops of every thread, or a negative
+ * value on error. */
 double ossl_esp_batch_decrypt(int alg, int nsa, const uint8_t *ckeys, int cklen, const uint8_t *akeys,
-                              int aklen, const uint8_t *salts, int mlen, uint8_t *arena,
+                              int aklen, const uint8_t *salts, int mlen, const uint8_t *arena, uint8_t *out,
                               const uint32_t *off4, const uint16_t *len, const uint16_t *sa_idx,
-                              uint8_t *status, uint32_t n, int nthreads) {
-  if (nthreads < 1 || nsa < 1 || (alg != 0 && alg != 1) || mlen < 4 || mlen > 20) return -1.0;
+                              uint8_t *status, uint32_t n, int nthreads, int reps) {
+  if (nthreads < 1 || nsa < 1 || (alg != 0 && alg != 1) || mlen < 4 || mlen > 20 || reps < 1 ||
+      (reps > 1 && out == arena))
+    return -1.0;
   pthread_t *th = calloc((size_t)nthreads, sizeof(*th));
   struct job *jobs = calloc((size_t)nthreads, sizeof(*jobs));
   pthread_barrier_t bar;
@@ -144,7 +152,7 @@ double ossl_esp_batch_decrypt(int alg, int nsa, const uint8_t *ckeys, int cklen,
     struct job *j = &jobs[t];
     j->alg = alg, j->nsa = nsa, j->cklen = cklen, j->aklen = aklen, j->mlen = mlen;
     j->ckeys = ckeys, j->akeys = akeys, j->salts = salts;
-    j->arena = arena, j->off4 = off4, j->len = len, j->sa_idx = sa_idx, j->status = status;
+    j->arena = arena, j->out = out, j->reps = reps, j->off4 = off4, j->len = len, j->sa_idx = sa_idx, j->status = status;
     j->lo = (uint32_t)((uint64_t)n * (uint64_t)t / (uint64_t)nthreads);
     j->hi = (uint32_t)((uint64_t)n * (uint64_t)(t + 1) / (uint64_t)nthreads);
     j->bar = &bar;

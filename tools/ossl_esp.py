@@ -22,12 +22,15 @@ def lib():
         f = _lib.ossl_esp_batch_decrypt
         f.restype = C.c_double
         f.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int,
-                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
+                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                      C.c_int, C.c_int]
     return _lib
 
 
-def batch_decrypt(alg, ckeys, arena, off4, lens, sa_idx, akeys=None, salts=None, mlen=16, nthreads=1):
-    """Decrypt records of `arena` (numpy uint8, modified in place).
+def batch_decrypt(alg, ckeys, arena, off4, lens, sa_idx, akeys=None, salts=None, mlen=16, nthreads=1,
+                  out=None, reps=1):
+    """Decrypt records of `arena` (numpy uint8): in place, or with `out` (same
+    size) to the same offsets of out, `reps` times over (out of place only).
     alg 'gcm': ckeys = AES keys (one per SA), salts = 4-byte salts;
     alg 'cbc_sha1': ckeys = AES keys, akeys = HMAC keys (20 B each).
     -> (seconds, status array: 0 ok, 74 EBADMSG, 22 EINVAL)."""
@@ -50,9 +53,12 @@ def batch_decrypt(alg, ckeys, arena, off4, lens, sa_idx, akeys=None, salts=None,
     assert arena.dtype == np.uint8 and arena.flags.c_contiguous
     n = len(off4)
     status = np.zeros(n, dtype=np.uint8)
-    t = lib().ossl_esp_batch_decrypt(a, nsa, ck, cklen, ak, aklen, sl, mlen, arena.ctypes.data,
+    if out is None:
+        out = arena
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= arena.size
+    t = lib().ossl_esp_batch_decrypt(a, nsa, ck, cklen, ak, aklen, sl, mlen, arena.ctypes.data, out.ctypes.data,
                                      off4.ctypes.data, lens.ctypes.data, sa_idx.ctypes.data,
-                                     status.ctypes.data, n, nthreads)
+                                     status.ctypes.data, n, nthreads, reps)
     if t < 0:
         raise RuntimeError("ossl_esp_batch_decrypt failed")
     return t, status
