@@ -63,6 +63,7 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #define ETA_HMAC_PREFETCH 0
 #endif
 
+
 constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
 // MODE 2 / 3 session sets (the CKS template argument): every ETA session, or
 // split by hash so that the common kernel carries no SHA-512 code (its
@@ -509,6 +510,33 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
   for (int k = 0; k < 8; ++k) out[k] = h[k];
 }
 
+// One block of hmac_t's loop (block b of the inner message, its padding, or
+// b == total: the outer block from the opad state), for callers that
+// interleave the hash with other work (MODE 7).
+template <int HS>
+__device__ __forceinline__ void hmac_step(uint32_t h[8], const uint8_t *rec, uint32_t b, uint32_t nfull,
+                                          uint32_t total, uint32_t L0, uint32_t L, bool esn, uint32_t esn_hi,
+                                          uint64_t bits, kptr opad) {
+  constexpr int W = Hash<HS>::W;
+  uint32_t w[16];
+  if (b < nfull) {
+    const uint8_t *q = rec + 64 * b;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = bswap4(ld16(q + 16 * k));
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+  } else if (b < total) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
+  } else {
+    outer_block<HS>(h, w);
+#pragma unroll
+    for (int k = 0; k < W; ++k) h[k] = opad[k];
+  }
+  Hash<HS>::compress(h, w);
+}
+
 // ---- SHA-512 / SHA-384 compression (SHA512_Transform, freebsd/crypto/sha2/sha512c.c:196) ----
 // 64-bit words held as uint64_t; rotations as two v_alignbit on the halves.
 __constant__ uint64_t kK512[80] = ESPGPU_SHA512_K;
@@ -847,6 +875,122 @@ __device__ __forceinline__ void fill_pair(uint8_t *lds, uint32_t base, const uin
   }
 }
 
+// MODE 7 (out of place, one session per wave unit, HMAC-SHA1 / SHA2-256 or no
+// authentication): the verify pass and the block-parallel decrypt run
+// interleaved in one loop instead of one after the other.  Out of place the
+// plaintext of a record that fails verification is not used (its status says
+// EBADMSG, its trailer word is 0), so every valid record is decrypted without
+// waiting for its HMAC, as the GCM kernel's MODE 0 does.  Iteration it issues
+// decrypt pass it's loads, runs HMAC block it of every lane's record (lane =
+// record, VALU; its own loads wait behind the pass's), then pass it's AES
+// rounds (LDS) and stores: each phase's memory latency hides under the other
+// phase's work, and the wave keeps both the VALU and the LDS pipe busy.
+// Returns the lane's verification result.
+template <int HS>
+__device__ __forceinline__ bool eta_interleaved(const EtaParams &p, const uint8_t *lds, uint32_t slot, int lane,
+                                                bool run, uint32_t off, uint32_t plen, uint32_t hl, uint32_t di,
+                                                uint32_t salt, uint32_t esnh, const DevSA *s) {
+  constexpr int U = 4;                                         // aes_dec4 / aes_enc4 width
+  const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM, null = s->calg == ESPGPU_CRYPTO_NULL_CBC;   // wave-uniform
+  const int nr = (int)s->nr;
+  const uint32_t aalg = s->aalg, mlen = s->mlen;
+  const uint8_t *rec = p.arena + off;
+  // flat block list of the wave's records
+  const uint32_t nb = run ? (plen + 15) / 16 : 0;
+  uint32_t incl = nb;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const uint32_t start = incl - nb;
+  const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
+  const int passes = (total + 64 * U - 1) / (64 * U);
+  // HMAC of rec[0, hl + plen) (|| ESN high word), hmac_t's block schedule
+  const bool esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
+  const uint32_t L0 = hl + plen, L = L0 + (esn ? 4u : 0u);
+  const uint32_t nfull = L0 / 64, htotal = (L + 9 + 63) / 64;
+  const uint64_t bits = (uint64_t)(64 + L) * 8;
+  const int hsteps = run && aalg != 0 ? (int)htotal + 1 : 0;
+  int hmax = hsteps;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) hmax = max(hmax, __shfl_xor(hmax, o));
+  uint32_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = k < Hash<HS>::W ? kp(s->ipad)[k] : 0u;
+  const int iters = max(passes, hmax);
+  for (int it = 0; it < iters; ++it) {
+    // (1) this pass's loads: blocks it*256 + lane + 64k of the flat list
+    int fk[U];
+    uint32_t ik[U], rok[U], rplk[U], rdik[U];
+    uint4 v[U], pv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int f = it * 64 * U + lane + 64 * k;
+      int j = 0;
+      uint32_t sj = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t sc = __shfl(start, j + step);
+        if ((int)sc <= f) {
+          j += step;
+          sj = sc;
+        }
+      }
+      fk[k] = f < total ? f : -1;
+      ik[k] = (uint32_t)f - sj;
+      rok[k] = __shfl(off, j);
+      rplk[k] = __shfl(plen, j);
+      rdik[k] = __shfl(di, j);
+      const uint32_t rs = __shfl(salt, j);
+      v[k] = pv[k] = make_uint4(0, 0, 0, 0);
+      if (fk[k] >= 0) {
+        const uint8_t *r = p.arena + rok[k];
+        if (null) {
+          v[k] = ld16(r + 8 + 16 * ik[k]);
+        } else if (ctr) {
+          pv[k] = ld16(r + 16 + 16 * ik[k]);
+          v[k] = make_uint4(rs, *reinterpret_cast<const uint32_t *>(r + 8),
+                            *reinterpret_cast<const uint32_t *>(r + 12), bswap32(ik[k] + 1));
+        } else {
+          v[k] = ld16(r + 24 + 16 * ik[k]);
+          pv[k] = ld16(r + 8 + 16 * ik[k]);
+        }
+      }
+    }
+    // (2) one HMAC block per lane
+    if (it < hsteps) hmac_step<HS>(h, rec, (uint32_t)it, nfull, htotal, L0, L, esn, esnh, bits, kp(s->opad));
+    // (3) the pass's rounds and stores
+    if (it < passes) {
+      if (null) {
+      } else if (ctr) {
+        aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
+      } else {
+        aes_dec4(v, kp(s->dk), nr, lds, slot);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (fk[k] >= 0) {
+          uint8_t *dst = p.out + rok[k];
+          const uint32_t i = ik[k], rpl = rplk[k];
+          const int rem = (int)rpl - 16 * (int)i;
+          const uint4 pt = xor4(v[k], pv[k]);
+          if (null) st_partial(dst + 8 + 16 * i, pt, rem);
+          else if (ctr) st_partial(dst + 16 + 16 * i, pt, rem);
+          else st16(dst + 24 + 16 * i, pt);
+          if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdik[k]] = esp_trailer_word(last_word(pt, rem), rpl);
+        }
+      }
+    }
+  }
+  if (!run) return false;
+  if (aalg == 0) return true;                                  // CSP_MODE_CIPHER: nothing to verify
+  uint32_t diff = 0;
+  for (uint32_t k = 0; k < mlen / 4; ++k)
+    diff |= bswap32(h[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
+  return diff == 0;
+}
+
 // MODE 0: decrypt out-of-place, one fused pass (SHA-1 / SHA2-256 sessions of
 // one cipher; used only with set_tuning eta_fused = 1); 1: encrypt in place,
 // MAC pass; 2: decrypt in place (verify first); 3: decrypt out of place,
@@ -928,7 +1072,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         have = false;                                       // the fused launches' session
       } else if ((MODE == 5 || MODE == 6) && two_pass_only(s->calg, s->aalg)) {
         have = false;                                       // MODE 3's session
-      } else if ((MODE == 2 || MODE == 3) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
+      } else if ((MODE == 2 || MODE == 3 || MODE == 7) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
                                               (CKS == CK_WIDEH && !wide_hash(s->aalg)))) {
         have = false;                                       // the other hash set's launch
       } else {
@@ -942,7 +1086,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         valid = pl > 0 && (ctr || null || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
         if (valid && MODE == 5) ok = p.status[di] == ESPGPU_OK;   // verified by the MODE 6 pass
-        if (valid && (MODE == 2 || MODE == 3) && s->aalg == 0) {
+        if (valid && (MODE == 2 || MODE == 3 || MODE == 7) && s->aalg == 0) {
           ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
         } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
@@ -1055,6 +1199,35 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       if (have && p.trailer && !valid) p.trailer[di] = 0;
       continue;
     }
+    if (MODE == 7) {
+      // one session in the unit (planner chunks): verify and decrypt
+      // interleaved; otherwise verify here and take MODE 3's path below
+      const bool run = have && valid;
+      const uint64_t rm = __ballot(run);
+      const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, rm ? __builtin_ctzll(rm) : 0));
+      if (rm && __all(!run || sa == sau)) {
+        const DevSA *s = p.sas + sau;
+        const bool good = s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC
+                              ? eta_interleaved<HS_SHA256>(p, lds, slot, lane, run, off, plen, hl, di, salt, esnh, s)
+                              : eta_interleaved<HS_SHA1>(p, lds, slot, lane, run, off, plen, hl, di, salt, esnh, s);
+        if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (good ? ESPGPU_OK : ESPGPU_EBADMSG);
+        if (have && p.trailer && !(valid && good)) p.trailer[di] = 0;
+        continue;
+      }
+      if (run && p.sas[sa].aalg != 0) {
+        const DevSA *s = p.sas + sa;
+        uint32_t dg[16];
+        const uint8_t *rec = p.arena + off;
+        if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+          hmac_t<HS_SHA256>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad), kp(s->opad), dg);
+        else
+          hmac_t<HS_SHA1>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad), kp(s->opad), dg);
+        uint32_t diff = 0;
+        for (uint32_t k = 0; k < s->mlen / 4; ++k)
+          diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
+        ok = diff == 0;
+      }
+    }
     if (MODE == 6) {                // verify pass: status only; MODE 5 decrypts what passed
       if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
       continue;
@@ -1147,7 +1320,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
           if (fk[k] >= 0) {
-            uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3 / 5: p.out (may be p.arena)
+            uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3 / 5 / 7: p.out (may be p.arena)
             const uint32_t i = ik[k], rpl = rplk[k];
             const int rem = (int)rpl - 16 * (int)i;
             const uint4 pt = xor4(v[k], pv[k]);
@@ -1210,7 +1383,10 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
       hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else if (p.two_pass_all) {
-      hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
+      if (p.interleave)
+        hipLaunchKernelGGL((eta_kernel<7, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
+      else
+        hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else {
       if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);

@@ -152,7 +152,8 @@ struct espgpu_ctx {
   // then the block-parallel decrypt of the verified records into out; cfg3
   // 2.39-2.45 ms), in place MODE 2 (2.44 ms); 1 = out of place one fused pass
   // per cipher (MODE 0, 2.53-2.55 ms); 0 = separate verify and decrypt
-  // kernels (2.52 / 2.55 ms)
+  // kernels (2.52 / 2.55 ms); 3 = out of place the verify and decrypt passes
+  // interleaved in one loop per wave (MODE 7), in place as 2
   int eta_fused = 2;
   // GCM lanes per record: 0 = by batch size, 4 or 8 forced (set_tuning
   // "gcm_lanes": the tests run both kernels at every batch size)
@@ -440,7 +441,8 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.nsas = nsas;
     const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wcbc > 0 ? 4 : 0) |
                    (c->n_wctr > 0 ? 8 : 0) | (c->n_whash > 0 ? 16 : 0);
-    q.two_pass_all = c->eta_fused == 2;
+    q.two_pass_all = c->eta_fused >= 2;
+    q.interleave = c->eta_fused == 3;
     if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, c->eta_fused != 0, st))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
@@ -1338,7 +1340,7 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
   if (!strcmp(key, "eta_fused")) {
-    if (value < 0 || value > 2) return ESPGPU_EINVAL;
+    if (value < 0 || value > 3) return ESPGPU_EINVAL;
     c->eta_fused = value;
     return 0;
   }

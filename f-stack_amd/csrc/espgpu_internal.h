@@ -118,6 +118,8 @@ struct EtaParams {
   uint8_t *status;
   uint32_t nsas;
   uint32_t two_pass_all;           // out of place: MODE 3 serves every ETA session (eta_fused 2)
+  uint32_t interleave;             // out of place: MODE 7 (verify and decrypt interleaved) instead of MODE 3's
+                                   // SHA-1 / SHA2-256 launch (eta_fused 3)
 };
 
 // esp_input_cb's checks on the last 3 plaintext bytes (xform_esp.c:597-630),

@@ -338,7 +338,8 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *               by gcm_split; others EINVAL;
  *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
  *               decrypt (MODE 3) out of place, 1 one fused pass per record
- *               (MODE 0), 0 separate verify / decrypt kernels; others EINVAL;
+ *               (MODE 0), 0 separate verify / decrypt kernels, 3 verify and
+ *               decrypt interleaved per wave out of place (MODE 7); others EINVAL;
  *   "overflow_mb" host overflow for process() while every staging slot is
  *               in flight, in MiB (0, the default: ERESTART; 0..65536);
  *   "xfer"      small batches' staging region moved by the xfer kernel (1,

@@ -224,7 +224,7 @@ def _mask_var(descs, size, hl, ml):
     return m
 
 
-@pytest.mark.parametrize("fused", [2, 1, 0])
+@pytest.mark.parametrize("fused", [2, 3, 1, 0])
 @pytest.mark.parametrize("esn", [False, True])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
@@ -232,8 +232,9 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
     batch (planner path), AES-128/192/256, tag failures anywhere in the
     record: statuses and plaintext bit-exact vs the oracle, failed records
     untouched in place.  fused (set_tuning eta_fused): 2 = the default
-    two-pass MODE 3 kernel out of place, 1 = the one-pass fused MODE 0
-    kernels, 0 = the separate verify + block-decrypt kernels."""
+    two-pass MODE 3 kernel out of place, 3 = verify and decrypt interleaved
+    (MODE 7), 1 = the one-pass fused MODE 0 kernels, 0 = the separate
+    verify + block-decrypt kernels."""
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
     try:
         _eta_variants_decrypt(drv, esn, inplace)
@@ -318,7 +319,7 @@ def test_eta_full_hash_icv_vs_oracle(drv, inplace):
 
 
 def test_eta_fused_knob_range(drv):
-    for v in (-1, 3, 7):
+    for v in (-1, 4, 7):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == 22
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
 
@@ -388,11 +389,22 @@ def test_eta_variants_encrypt_vs_oracle(drv):
         drv.freesession(s)
 
 
-def test_eta_variants_trailer(drv):
+@pytest.mark.parametrize("fused", [2, 3])
+def test_eta_variants_trailer(drv, fused):
     """The fused esp_input_cb trailer word for CTR records (partial last
-    block) and SHA2-256 sessions, out of place and in place."""
+    block) and SHA2-256 sessions, out of place and in place; a record whose
+    ICV fails gets EBADMSG and trailer word 0 (eta_fused 3 decrypts it out of
+    place before its HMAC is known)."""
     from espgpu.batch import decrypt_batch
     from espgpu.esp import trailer_word
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
+    try:
+        _eta_variants_trailer(drv, decrypt_batch, trailer_word)
+    finally:
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+
+
+def _eta_variants_trailer(drv, decrypt_batch, trailer_word):
     rng = np.random.default_rng(1500)
     sas = _variant_sas(rng)
     sids = _sessions(drv, sas)
@@ -407,14 +419,21 @@ def test_eta_variants_trailer(drv):
     hl, ml = _hl(sas, sa_idx)
     want = np.array([trailer_word(plain[int(o) * 4 + h:int(o) * 4 + int(L) - a])
                      for o, L, h, a in zip(descs["off4"], descs["len"], hl, ml)], dtype=np.uint32)
+    # every 7th authenticated record: a flipped ICV bit
+    bad = ct.copy()
+    flip = np.array([i % 7 == 3 and ml[i] > 0 for i in range(n)])
+    for i in np.flatnonzero(flip):
+        bad[int(descs["off4"][i]) * 4 + int(descs["len"][i]) - 1] ^= 0x01
+    want[flip] = 0
     for inplace in (False, True):
-        arena = _dev(ct)
+        arena = _dev(bad)
         out = arena if inplace else torch.zeros_like(arena)
         st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
         trl = torch.zeros(n, dtype=torch.int32, device="cuda")
         decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None if inplace else out, grouped=False, trailer=trl)
         torch.cuda.synchronize()
-        assert (st.cpu().numpy() == 0).all()
+        got = st.cpu().numpy()
+        assert (got[flip] == 74).all() and (got[~flip] == 0).all()
         assert (trl.cpu().numpy().view(np.uint32) == want).all(), inplace
     for s in sids:
         drv.freesession(s)
