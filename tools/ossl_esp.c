@@ -37,7 +37,7 @@ struct job {
   const uint16_t *len, *sa_idx;
   uint8_t *status;
   uint32_t lo, hi;
-  pthread_barrier_t *bar;
+  double t0, t1;   // the record loop's start and end (CLOCK_MONOTONIC)
   int err;
 };
 
@@ -79,6 +79,12 @@ static uint8_t eta_one(EVP_CIPHER_CTX *c, HMAC_CTX *h, const uint8_t *rec, uint8
   return ST_OK;
 }
 
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
 static void *worker(void *arg) {
   struct job *j = (struct job *)arg;
   EVP_CIPHER_CTX **cc = calloc((size_t)j->nsa, sizeof(*cc));
@@ -102,7 +108,7 @@ static void *worker(void *arg) {
     }
   }
   if (!cc || !hh) j->err = 1;
-  pthread_barrier_wait(j->bar);
+  j->t0 = now_s();
   for (int r = 0; r < j->reps && !j->err; ++r) {
     for (uint32_t i = j->lo; i < j->hi; ++i) {
       const int s = j->sa_idx[i];
@@ -112,7 +118,7 @@ static void *worker(void *arg) {
                                  : eta_one(cc[s], hh[s], j->arena + o, j->out + o, j->len[i], j->mlen);
     }
   }
-  pthread_barrier_wait(j->bar);
+  j->t1 = now_s();
   for (int s = 0; s < j->nsa && cc && hh; ++s) {
     EVP_CIPHER_CTX_free(cc[s]);
     if (hh[s]) HMAC_CTX_free(hh[s]);
@@ -122,17 +128,11 @@ static void *worker(void *arg) {
   return NULL;
 }
 
-static double now_s(void) {
-  struct timespec t;
-  clock_gettime(CLOCK_MONOTONIC, &t);
-  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
-}
-
 /* Decrypts n records with nthreads threads (contiguous record ranges), reps
  * times over: plaintext to the same offsets of `out` (out == arena: in
- * place; then reps must be 1); fills status.  Returns the seconds between the
- * two barriers that bracket the record loops of every thread, or a negative
- * value on error. */
+ * place; then reps must be 1); fills status.  Returns the seconds from the
+ * first thread's start of its record loop to the last one's end (session
+ * setup excluded), or a negative value on error. */
 double ossl_esp_batch_decrypt(int alg, int nsa, const uint8_t *ckeys, int cklen, const uint8_t *akeys,
                               int aklen, const uint8_t *salts, int mlen, const uint8_t *arena, uint8_t *out,
                               const uint32_t *off4, const uint16_t *len, const uint16_t *sa_idx,
@@ -142,12 +142,12 @@ double ossl_esp_batch_decrypt(int alg, int nsa, const uint8_t *ckeys, int cklen,
     return -1.0;
   pthread_t *th = calloc((size_t)nthreads, sizeof(*th));
   struct job *jobs = calloc((size_t)nthreads, sizeof(*jobs));
-  pthread_barrier_t bar;
-  if (!th || !jobs || pthread_barrier_init(&bar, NULL, (unsigned)nthreads + 1) != 0) {
+  if (!th || !jobs) {
     free(th);
     free(jobs);
     return -1.0;
   }
+  int made = 0, err = 0;
   for (int t = 0; t < nthreads; ++t) {
     struct job *j = &jobs[t];
     j->alg = alg, j->nsa = nsa, j->cklen = cklen, j->aklen = aklen, j->mlen = mlen;
@@ -155,19 +155,19 @@ double ossl_esp_batch_decrypt(int alg, int nsa, const uint8_t *ckeys, int cklen,
     j->arena = arena, j->out = out, j->reps = reps, j->off4 = off4, j->len = len, j->sa_idx = sa_idx, j->status = status;
     j->lo = (uint32_t)((uint64_t)n * (uint64_t)t / (uint64_t)nthreads);
     j->hi = (uint32_t)((uint64_t)n * (uint64_t)(t + 1) / (uint64_t)nthreads);
-    j->bar = &bar;
-    pthread_create(&th[t], NULL, worker, j);
+    if (pthread_create(&th[t], NULL, worker, j) != 0) {
+      err = 1;   // the threads already running finish and are joined
+      break;
+    }
+    ++made;
   }
-  pthread_barrier_wait(&bar);
-  const double t0 = now_s();
-  pthread_barrier_wait(&bar);
-  const double t1 = now_s();
-  int err = 0;
-  for (int t = 0; t < nthreads; ++t) {
+  double t0 = 0, t1 = 0;
+  for (int t = 0; t < made; ++t) {
     pthread_join(th[t], NULL);
     err |= jobs[t].err;
+    if (t == 0 || jobs[t].t0 < t0) t0 = jobs[t].t0;
+    if (t == 0 || jobs[t].t1 > t1) t1 = jobs[t].t1;
   }
-  pthread_barrier_destroy(&bar);
   free(th);
   free(jobs);
   return err ? -1.0 : t1 - t0;
