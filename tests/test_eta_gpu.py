@@ -637,3 +637,44 @@ def test_grouped_mode_mixed_run_fails_closed(drv):
     assert (res[m] == plain[m]).all()
     for s in sids:
         drv.freesession(s)
+
+
+@pytest.mark.parametrize("fused", [2, 3])
+def test_eta_mixed_sessions_in_one_wave_unit(drv, fused):
+    """Caller-grouped batch whose 64-record units mix ETA sessions (CBC +
+    HMAC-SHA1, CTR + HMAC-SHA2-256, CBC + HMAC-SHA2-384): eta_fused 3 takes
+    MODE 7's per-lane fallback (verify, then MODE 3's verified decrypt) for
+    such units, the wide-hash records go to their own launch; statuses and
+    verified plaintext vs the oracle, out of place, with tampered ICVs."""
+    from espgpu.batch import decrypt_batch
+    rng = np.random.default_rng(1900 + fused)
+    sas = [EtaSA(rng, 16), EtaSA(rng, 32, ctr=True, sha256=True), EtaSA(rng, 24, sha=384)]
+    sids = _sessions(drv, sas)
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
+    try:
+        n = 640
+        kinds = rng.integers(0, 3, n)
+        cts = rng.choice([16, 208, 1440], n)
+        plain, ct, descs, eh = build_records(rng, sas, kinds, cts)
+        bad = ct.copy()
+        flip = rng.random(n) < 0.1
+        for i in np.flatnonzero(flip):
+            bad[int(descs["off4"][i]) * 4 + int(descs["len"][i]) - 1] ^= 0x02
+        ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+        assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+        d = descs.copy()
+        d["sa"] = [sids[k] for k in kinds]
+        arena, out = _dev(bad), torch.zeros(len(bad), dtype=torch.uint8, device="cuda")
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        decrypt_batch(drv, arena, _descs_dev(d), n, st, out=out, grouped=True)
+        torch.cuda.synchronize()
+        got = st.cpu().numpy()
+        assert (got == ref_st).all(), np.flatnonzero(got != ref_st)[:10]
+        hl, ml = _hl(sas, kinds)
+        ok = got == 0
+        m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
+        assert (out.cpu().numpy()[m_ok] == plain[m_ok]).all()
+    finally:
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+        for s in sids:
+            drv.freesession(s)
