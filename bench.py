@@ -135,6 +135,8 @@ def main():
                     help="experiment: override the config's SA count (0 = the config's own)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive host-to-host leg")
     ap.add_argument("--e2e-chunk", type=int, default=65536, help="records per pipelined step")
+    ap.add_argument("--out-pad", type=int, default=0,
+                    help="experiment: extra bytes per record in the out-of-place buffer (layout probes)")
     args = ap.parse_args()
 
     import torch
@@ -200,7 +202,7 @@ def main():
     encrypt_batch(drv, arena, desc, n, status, grouped=grouped)     # build valid ESP records (untimed)
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0, "record generation failed"
-    out = None if args.inplace else torch.empty_like(arena)
+    out = None if args.inplace else torch.empty(total + args.out_pad * n, dtype=torch.uint8, device=dev)
     pristine = arena.clone() if args.inplace else None
     rec_bytes = int(d["len"].astype(np.int64).sum())
     pkt_bytes = int(sizes.astype(np.int64).sum())

@@ -73,6 +73,9 @@
 #ifndef GCM_ALIGNED
 #define GCM_ALIGNED 1
 #endif
+#ifndef GCM_OUTALIGN
+#define GCM_OUTALIGN 0
+#endif
 
 namespace espgpu {
 
@@ -581,7 +584,14 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     return;
   }
   const uint32_t rk3 = rk[3];
+#if GCM_OUTALIGN
+  // layout probe (tools/outalign_ab.sh, bench.py --out-pad 40; cfg1's
+  // 1500-byte slots only, results land elsewhere): record k's plaintext at
+  // out + k*1536 + 128, so every 128-byte line is written whole
+  uint8_t *orec = (MODE == 0 ? p.out + ((size_t)(rec - p.arena) / 1500) * 1536 + 112 : rec);
+#else
   uint8_t *orec = (MODE == 0 ? p.out - p.arena + rec : rec);
+#endif
   CtrCache cc;
   cc.hi = -1;                                               // built on first use
 
