@@ -1211,7 +1211,12 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
                               ? eta_interleaved<HS_SHA256>(p, lds, slot, lane, run, off, plen, hl, di, salt, esnh, s)
                               : eta_interleaved<HS_SHA1>(p, lds, slot, lane, run, off, plen, hl, di, salt, esnh, s);
         if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (good ? ESPGPU_OK : ESPGPU_EBADMSG);
-        if (have && p.trailer && !(valid && good)) p.trailer[di] = 0;
+        if (p.trailer) {
+          // another lane of this wave may have written the record's trailer
+          // word in a decrypt pass: order that store before the zeroing
+          __threadfence_block();
+          if (have && !(valid && good)) p.trailer[di] = 0;
+        }
         continue;
       }
       if (run && p.sas[sa].aalg != 0) {
