@@ -588,7 +588,9 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   // layout probe (tools/outalign_ab.sh, bench.py --out-pad 40; cfg1's
   // 1500-byte slots only, results land elsewhere): record k's plaintext at
   // out + k*1536 + 128, so every 128-byte line is written whole
-  uint8_t *orec = (MODE == 0 ? p.out + ((size_t)(rec - p.arena) / 1500) * 1536 + 112 : rec);
+  // (GCM_OUTALIGN - 1: extra bytes past the line start, to separate the
+  // 16-byte alignment of the stores from the line completion)
+  uint8_t *orec = (MODE == 0 ? p.out + ((size_t)(rec - p.arena) / 1500) * 1536 + 112 + (GCM_OUTALIGN - 1) : rec);
 #else
   uint8_t *orec = (MODE == 0 ? p.out - p.arena + rec : rec);
 #endif
