@@ -129,6 +129,8 @@ def main():
                          "with the in-place rate reported beside it)")
     ap.add_argument("--no-inplace-leg", action="store_true", help="skip the in-place side measurement")
     ap.add_argument("--no-encrypt-leg", action="store_true", help="skip the encrypt-direction side measurement")
+    ap.add_argument("--no-packed-leg", action="store_true",
+                    help="skip the packed-output side measurement (espgpu_decrypt_batch_packed)")
     ap.add_argument("--tuning", action="append", default=[],
                     help="experiment: espgpu_set_tuning key=value (e.g. grid=300; gcm_opts and eta_opts need the knobs build)")
     ap.add_argument("--nsa", type=int, default=0,
@@ -278,6 +280,10 @@ def main():
         result["inplace"] = inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes,
                                         algo_bytes, world, dist, launched_kernel(cfg, True))
 
+    if not args.inplace and not args.no_packed_leg and cfg["alg"] == "gcm":
+        result["packed_out"] = packed_leg(drv, arena, desc, d, n, status, grouped, stream, pkt_bytes,
+                                          algo_bytes, world, dist)
+
     if not args.inplace and not args.no_encrypt_leg:
         result["encrypt"] = encrypt_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, world, dist, cfg)
 
@@ -371,6 +377,40 @@ def inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, algo_by
             "achieved_algorithmic_GBps": round(algo_bytes / (ms * 1e-3) / 1e9, 1),
             "status_ok": ok, "timing": "median of %d launches, HIP events around the decrypt only" % reps,
             "kernel": kernel + " (verify-first, in place)"}
+
+
+def packed_leg(drv, arena, desc, d, n, status, grouped, stream, pkt_bytes, algo_bytes, world, dist):
+    """The same out-of-place decrypt with a packed output
+    (espgpu_decrypt_batch_packed: record i's plaintext at out + i*stride,
+    stride = the largest payload rounded up to 128 bytes, every output line
+    written whole), beside the headline's record layout; not the headline."""
+    import torch
+    from espgpu.batch import decrypt_batch_packed
+    ct_max = int(d["len"].max()) - HDR_TRAILER["gcm"]
+    stride = (ct_max + 127) // 128 * 128
+    out = torch.empty(n * stride, dtype=torch.uint8, device=arena.device)
+    reps = 5
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps + 1)]
+    with torch.cuda.stream(stream):
+        for e0, e1 in evs:
+            e0.record(stream)
+            decrypt_batch_packed(drv, arena, desc, n, status, out, stride, grouped=grouped, stream=stream)
+            e1.record(stream)
+    torch.cuda.synchronize()
+    ok = int((status != 0).sum()) == 0
+    ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs[1:])[reps // 2]
+    del out
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64, device=arena.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        b = torch.tensor([float(pkt_bytes)], dtype=torch.float64, device=arena.device)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        ms, pkt_bytes = float(t.item()), float(b.item())
+    return {"value": round(pkt_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "kernel_ms": round(ms, 4),
+            "achieved_algorithmic_GBps": round(algo_bytes / (ms * 1e-3) / 1e9, 1),
+            "frac": round(algo_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "out_stride": stride,
+            "status_ok": ok, "timing": "median of %d launches, HIP events around the decrypt only" % reps,
+            "api": "espgpu_decrypt_batch_packed (plaintext of record i at out + i*stride; not the headline)"}
 
 
 def encrypt_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, world, dist, cfg):

@@ -557,7 +557,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
     len = dv.y & 0xffffu;
     ct_len = (int)len - 16 - (int)mlen;                      // 8 hdr + 8 IV + ICV
-    valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;   // xform_esp.c:279-324
+    valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0 &&   // xform_esp.c:279-324
+            (MODE != 0 || p.out_stride == 0 || ct_len <= (int)p.out_stride);   // packed output: fits its slot
     if (valid) {
       rec = p.arena + (size_t)dv.x * 4;
       const uint4 h = ld16(rec);                             // SPI, SN, explicit IV
@@ -592,7 +593,11 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   // 16-byte alignment of the stores from the line completion)
   uint8_t *orec = (MODE == 0 ? p.out + ((size_t)(rec - p.arena) / 1500) * 1536 + 112 + (GCM_OUTALIGN - 1) : rec);
 #else
-  uint8_t *orec = (MODE == 0 ? p.out - p.arena + rec : rec);
+  // out of place: the record's own offset in out, or (packed output) slot di
+  // of out_stride bytes; orec is where the record's header would be, the
+  // plaintext starts 16 bytes after it
+  uint8_t *orec = (MODE == 0 ? (p.out_stride ? p.out + (size_t)di * p.out_stride - 16 : p.out - p.arena + rec)
+                             : rec);
 #endif
   CtrCache cc;
   cc.hi = -1;                                               // built on first use

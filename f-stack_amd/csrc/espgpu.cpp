@@ -372,8 +372,11 @@ struct StageLists {
 
 int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
               uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st,
-              uint32_t *d_trailer = nullptr, uint32_t kinds = 3, const StageLists *stage = nullptr) {
+              uint32_t *d_trailer = nullptr, uint32_t kinds = 3, const StageLists *stage = nullptr,
+              uint32_t out_stride = 0) {
   if (n == 0) return 0;
+  if (out_stride && c->n_eta > 0)
+    return fail(c, ESPGPU_ENOTSUP, "packed output serves contexts with GCM sessions only");
   if (c->launched && st != c->last_st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
   const uint32_t nsas = (uint32_t)c->sessions.size();
   GcmParams p{};
@@ -388,6 +391,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   p.nsas = nsas;
   p.queue = c->d_queue;
   p.trailer = encrypt ? nullptr : d_trailer;
+  p.out_stride = out_stride;
   if (stage) {
     p.xin = stage->xin;
     p.xout = stage->xout;
@@ -409,7 +413,9 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   // the burst kernel (small batches of <= gcm_burst records, out of place or
   // encrypt; launch_gcm picks the kernel from it)
   const bool gsmall = c->gcm_lanes ? c->gcm_lanes == kGcmLanesSmall : n < kGcmSmallBatch;
-  if ((kinds & 1) && (((c->gcm_split || c->gcm_bs) && !gsmall) || (gsmall && !two_pass && n <= c->gcm_burst))) {
+  // (packed output: the fused kernel only)
+  if ((kinds & 1) && !out_stride &&
+      (((c->gcm_split || c->gcm_bs) && !gsmall) || (gsmall && !two_pass && n <= c->gcm_burst))) {
     if (n > c->ej0_cap) {
       hipFree(c->d_ej0);
       c->d_ej0 = nullptr;
@@ -1275,6 +1281,16 @@ int espgpu_decrypt_batch_trailer(espgpu_ctx *c, uint8_t *d_arena, const espgpu_d
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_trailer && n)) return ESPGPU_EINVAL;
   return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
                    reinterpret_cast<hipStream_t>(stream), d_trailer);
+}
+
+int espgpu_decrypt_batch_packed(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
+                                uint8_t *d_status, uint8_t *d_out, uint32_t out_stride, uint32_t flags,
+                                void *stream) {
+  if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_out && n) || d_out == d_arena ||
+      out_stride == 0 || out_stride % 128 != 0)
+    return ESPGPU_EINVAL;
+  return run_batch(c, d_arena, d_desc, n, d_status, d_out, flags, 0, reinterpret_cast<hipStream_t>(stream),
+                   nullptr, 3, nullptr, out_stride);
 }
 
 int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,

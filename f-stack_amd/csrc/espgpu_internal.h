@@ -99,6 +99,9 @@ struct GcmParams {
   const struct XferSpan *xin, *xout;
   uint8_t *hstat;
   const espgpu_desc *hdesc;
+  // decrypt out of place: 0 = plaintext at the record's own offset in out;
+  // else record i's plaintext at out + i * out_stride (espgpu_decrypt_batch_packed)
+  uint32_t out_stride;
 };
 
 struct EtaParams {

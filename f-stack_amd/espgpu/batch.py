@@ -49,6 +49,19 @@ def decrypt_batch(driver, arena, desc, n, status, out=None, grouped=False, strea
         raise RuntimeError("espgpu_decrypt_batch: %s" % driver.last_error())
 
 
+def decrypt_batch_packed(driver, arena, desc, n, status, out, stride, grouped=False, stream=None):
+    """Verify+decrypt n GCM records, record i's plaintext to out[i*stride:]
+    (espgpu_decrypt_batch_packed: stride a multiple of 128, out of place)."""
+    for t in (arena, desc, status, out):
+        assert t.is_cuda and t.is_contiguous()
+    assert out.numel() >= n * stride
+    rc = driver.lib.espgpu_decrypt_batch_packed(
+        driver.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(), out.data_ptr(), stride,
+        L.BATCH_GROUPED if grouped else 0, _stream_ptr(stream))
+    if rc:
+        raise RuntimeError("espgpu_decrypt_batch_packed: %s (%d)" % (driver.last_error(), rc))
+
+
 def encrypt_batch(driver, arena, desc, n, status, grouped=False, stream=None):
     for t in (arena, desc, status):
         assert t.is_cuda and t.is_contiguous()

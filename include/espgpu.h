@@ -248,6 +248,18 @@ int  espgpu_decrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu
 int  espgpu_encrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
                           uint32_t n, uint8_t *d_status, uint32_t flags, void *stream);
 
+/* espgpu_decrypt_batch with a packed output: the plaintext (ESP payload) of
+ * record i lands at d_out + i * out_stride instead of the record's own offset,
+ * every 128-byte line of it written whole (out_stride a nonzero multiple of
+ * 128; d_out != d_arena, n * out_stride bytes).  A record whose payload is
+ * longer than out_stride is EINVAL.  For a device-side consumer of the
+ * plaintext; the line-aligned stores make the kernel ≈ 6 % faster than the
+ * record layout's.  GCM contexts only: ENOTSUP when the
+ * context has ETA sessions.  No esp_input_cb trailer words. */
+int  espgpu_decrypt_batch_packed(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
+                                 uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t out_stride,
+                                 uint32_t flags, void *stream);
+
 /* Decrypt + the ESP trailer checks of esp_input_cb (xform_esp.c:597-630)
  * fused into the kernels: d_trailer[i] (one 32-bit word per record) gets
  *   bits 0-7  next header, bits 8-15 pad length (the last 3 plaintext bytes),

@@ -677,3 +677,77 @@ def test_gcm_bs_knob_range(drv):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 22
     for v in (2, 1, 0):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 0
+
+
+@pytest.mark.parametrize("lanes", [0, 4, 8])
+@pytest.mark.parametrize("n,grouped", [(700, False), (40000, False), (40000, True)])
+def test_packed_output_vs_oracle(n, grouped, lanes):
+    """espgpu_decrypt_batch_packed: record i's plaintext at out + i*stride
+    (128-byte aligned), mixed sizes and sessions (planner) or one session
+    (caller-grouped), small (S = 8) and large batches; statuses and verified
+    plaintext vs the oracle, a record longer than the stride is EINVAL, the
+    bytes of each slot past its payload are never written."""
+    from espgpu.batch import decrypt_batch_packed
+    from espgpu.opencrypto import GpuCryptoDriver
+    d = GpuCryptoDriver(max_sessions=16)
+    try:
+        assert d.lib.espgpu_set_tuning(d.ctx, b"gcm_lanes", lanes) == 0      # 0: by batch size
+        rng = np.random.default_rng(2100 + n + grouped)
+        nsa = 1 if grouped else 3
+        sas = [GcmSA(rng, klen=16 + 8 * (i % 3), mlen=(16, 12, 8)[i % 3]) for i in range(nsa)]
+        sids = _sessions(d, sas)
+        sa_idx = np.zeros(n, dtype=np.int64) if grouped else rng.integers(0, nsa, n)
+        stride = 1536
+        cts = rng.choice([12, 204, 1448, 1452, 1536, 1540], n)     # 1540 > stride: EINVAL
+        plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts)
+        bad = ct.copy()
+        flip = rng.random(n) < 0.05
+        for i in np.flatnonzero(flip):
+            bad[int(descs["off4"][i]) * 4 + int(descs["len"][i]) - 1] ^= 0x10
+        ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+        want_st = np.where(cts > stride, O.EINVAL, ref_st)
+        dd = descs.copy()
+        dd["sa"] = [sids[s] for s in sa_idx]
+        arena = _dev(bad)
+        out = torch.full((n * stride,), 0xA5, dtype=torch.uint8, device="cuda")
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        decrypt_batch_packed(d, arena, _descs_dev(dd), n, st, out, stride, grouped=grouped)
+        torch.cuda.synchronize()
+        got = st.cpu().numpy()
+        assert (got == want_st).all(), np.flatnonzero(got != want_st)[:10]
+        res = out.cpu().numpy().reshape(n, stride)
+        for i in np.flatnonzero(got == 0):
+            o, L, ml = int(descs["off4"][i]) * 4, int(descs["len"][i]), sas[sa_idx[i]].mlen
+            c = L - 16 - ml
+            assert res[i, :c].tobytes() == plain[o + 16:o + 16 + c].tobytes(), i
+            assert (res[i, c:] == 0xA5).all(), i
+        for i in np.flatnonzero(cts > stride):
+            assert (res[i] == 0xA5).all(), i
+        for s in sids:
+            d.freesession(s)
+    finally:
+        d.close()
+
+
+def test_packed_output_rejects(drv):
+    """Stride not a multiple of 128, in place, or a context holding ETA
+    sessions: EINVAL / ENOTSUP."""
+    from espgpu.esp import CBC_SHA1, SecAssoc
+    z = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    dsc = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    L = drv.lib
+    assert L.espgpu_decrypt_batch_packed(drv.ctx, z.data_ptr(), dsc.data_ptr(), 1, st.data_ptr(), z.data_ptr(),
+                                         1536, 0, None) == 22
+    out = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    assert L.espgpu_decrypt_batch_packed(drv.ctx, z.data_ptr(), dsc.data_ptr(), 1, st.data_ptr(), out.data_ptr(),
+                                         1500, 0, None) == 22
+    assert L.espgpu_decrypt_batch_packed(drv.ctx, z.data_ptr(), dsc.data_ptr(), 1, st.data_ptr(), out.data_ptr(),
+                                         0, 0, None) == 22
+    rc, sid = drv.newsession(SecAssoc(0x4242, CBC_SHA1, bytes(16), bytes(20)).csp())
+    assert rc == 0
+    try:
+        assert L.espgpu_decrypt_batch_packed(drv.ctx, z.data_ptr(), dsc.data_ptr(), 1, st.data_ptr(),
+                                             out.data_ptr(), 1536, 0, None) == 95
+    finally:
+        drv.freesession(sid)

@@ -4,7 +4,7 @@
 #   bash tools/inplace_ab.sh <cfg> <lib1> <lib2> ... (run on the GPU box)
 set -e
 CFG=$1; shift
-B="python bench.py --config $CFG --inplace --steps 20 --warmup 10 --no-cpu --no-e2e --no-encrypt-leg"
+B="python bench.py --config $CFG --inplace --steps 20 --warmup 10 --no-cpu --no-e2e --no-encrypt-leg --no-packed-leg"
 for k in 1 2 3; do
   for L in "$@"; do
     echo -n "$L "

@@ -3,7 +3,7 @@
 # ms_per_step of each.   bash tools/lib_ab.sh <cfg> <lib1> <lib2> ... (run on the GPU box)
 set -e
 CFG=$1; shift
-B="python bench.py --config $CFG --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e --no-encrypt-leg"
+B="python bench.py --config $CFG --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e --no-encrypt-leg --no-packed-leg"
 for k in 1 2 3; do
   for L in "$@"; do
     echo -n "$L "

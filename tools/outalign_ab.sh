@@ -4,7 +4,7 @@
 # record k's plaintext at out + k*1536 + 128).
 #   bash tools/outalign_ab.sh <lib1> <lib2> ... (run on the GPU box)
 set -e
-B="python bench.py --config cfg1 --out-pad 40 --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e --no-encrypt-leg"
+B="python bench.py --config cfg1 --out-pad 40 --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e --no-encrypt-leg --no-packed-leg"
 for k in 1 2 3; do
   for L in "$@"; do
     echo -n "$L "

@@ -9,7 +9,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu --no-e2e --no-inplace-leg --no-encrypt-leg "$@")
+BENCH=(python3 "$ROOT/bench.py" --steps 20 --warmup 10 --no-cpu --no-e2e --no-inplace-leg --no-encrypt-leg --no-packed-leg "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/pmc_write.log" 2>&1

@@ -4,7 +4,7 @@
 #   bash tools/tuning_ab.sh <cfg> <key=value> <key=value> ... (run on the GPU box)
 set -e
 CFG=$1; shift
-B="python bench.py --config $CFG --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e --no-encrypt-leg"
+B="python bench.py --config $CFG --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e --no-encrypt-leg --no-packed-leg"
 for k in 1 2 3; do
   for T in "$@"; do
     echo -n "$T "
