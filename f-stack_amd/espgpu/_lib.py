@@ -136,7 +136,8 @@ def lib():
         L.espgpu_decrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint32, vp]
         L.espgpu_encrypt_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp]
         L.espgpu_decrypt_batch_trailer.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint32, vp]
-        L.espgpu_decrypt_batch_packed.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint32, C.c_uint32, vp]
+        if hasattr(L, "espgpu_decrypt_batch_packed"):   # (absent from older builds used in A/B runs)
+            L.espgpu_decrypt_batch_packed.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint32, C.c_uint32, vp]
         L.espgpu_replay_check_batch.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_uint32, vp, vp, vp]
         L.espgpu_replay_merge.argtypes = [vp, vp, vp, C.c_uint32, vp]
         L.espgpu_replay_update.argtypes = [C.POINTER(Replay), C.POINTER(C.c_uint32), C.c_uint32]
