@@ -69,7 +69,8 @@ constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
 // split by hash so that the common kernel carries no SHA-512 code (its
 // registers then fit without spilling): HMAC-SHA1 / SHA2-256 / none, or
 // HMAC-SHA2-384 / 512 only
-constexpr int CK_ALL = -1, CK_NARROW = -2, CK_WIDEH = -3;
+[[maybe_unused]] constexpr int CK_ALL = -1;                     // variants build only
+constexpr int CK_NARROW = -2, CK_WIDEH = -3;
 constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
 
 typedef const __attribute__((address_space(4))) uint32_t *kptr;
@@ -1387,18 +1388,26 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     if (in_place) {
       hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-    } else if (p.two_pass_all) {
-      if (p.interleave)
-        hipLaunchKernelGGL((eta_kernel<7, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
-      else
-        hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
+    } else if (p.two_pass_all && !p.interleave) {
+      hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else {
-      if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+#ifdef ESPGPU_VARIANTS
+      // measured-slower designs, variants library only
+      if (p.two_pass_all) {
+        hipLaunchKernelGGL((eta_kernel<7, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
+        if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      } else {
+        if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+        if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+        if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      }
+#else
+      return -1;
+#endif
     }
   } else {
+#ifdef ESPGPU_VARIANTS
     // verify pass (lane = record HMAC, status), then the block-parallel
     // decrypt of the records that passed, in place or out of place: two lean
     // kernels, each at the occupancy its own registers allow
@@ -1407,6 +1416,9 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
       hipLaunchKernelGGL((eta_kernel<5, 1024, -1>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
     }
     if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+#else
+    return -1;
+#endif
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

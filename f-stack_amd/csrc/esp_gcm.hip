@@ -44,8 +44,10 @@
 
 #include <algorithm>
 
-#include "aes_bs.h"
 #include "espgpu_internal.h"
+#ifdef ESPGPU_VARIANTS
+#include "aes_bs.h"
+#endif
 #include "xfer_copy.h"
 
 // Experiment switches (tools/variant.sh builds; defaults are the product)
@@ -1179,6 +1181,9 @@ __device__ __forceinline__ void tag_finish(const GcmParams &p, uint32_t di, uint
   if (p.trailer && !(valid && ok)) p.trailer[di] = 0;
 }
 
+#ifdef ESPGPU_VARIANTS
+// Measured-slower designs, built only into the variants
+// library (make -C f-stack_amd variants): the split design's two kernels.
 // KIND 0: the ctr pass (S = kCtrLanes, T-table in LDS); KIND 1: the tag pass
 // (S lanes per record, the H^S GHASH table in LDS).  Chunks, tickets and the
 // non-AEAD chunk rule as gcm_kernel.
@@ -1267,6 +1272,8 @@ void gcm_split_kernel(GcmParams p) {
     atomicExch(&p.queue[1], 0u);
   }
 }
+
+#endif  // ESPGPU_VARIANTS
 
 // Self-staging prologue of one chunk (gcm_kernel<..., STAGE>): copies the
 // chunk's descriptors (p.hdesc -> p.desc) and records (p.xin) from host memory
@@ -1596,6 +1603,7 @@ __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
   }
 }
 
+#ifdef ESPGPU_VARIANTS
 // ---- bitsliced ctr pass (aes_bs.h) -------------------------------------------
 // The split design's ctr pass with the AES on the VALU instead of the LDS
 // (the T-table kernels are bound by the LDS lookup rate).  A
@@ -1666,7 +1674,7 @@ void gcm_bsctr_kernel(GcmParams p) {
       const int ct_len = (int)len - 16 - (int)mlen;
       bool valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
       if (DIR == 2 && valid) valid = p.status[di] == ESPGPU_OK;
-      if (valid) nw = ((((uint32_t)ct_len + 15) >> 4) + 1 >> 5) + 1;   // counters 2 .. nct+1
+      if (valid) nw = (((((uint32_t)ct_len + 15) >> 4) + 1) >> 5) + 1;   // counters 2 .. nct+1
     }
     uint32_t v = nw;
 #pragma unroll
@@ -1831,6 +1839,8 @@ void gcm_bsctr_kernel(GcmParams p) {
   }
 }
 
+#endif  // ESPGPU_VARIANTS
+
 }  // namespace
 
 #ifdef ESPGPU_KNOBS
@@ -1847,6 +1857,7 @@ int set_gcm_opts(uint32_t opts) {
 #endif
 }
 
+#ifdef ESPGPU_VARIANTS
 // The split design for a large batch (ctr and tag passes, see gcm_split_kernel):
 // kernels on one stream, each resetting its ticket counters before the next starts.
 static int launch_gcm_split(const GcmParams &p, int encrypt, int two_pass, int grid, hipStream_t st) {
@@ -1901,6 +1912,8 @@ static int launch_gcm_bs(const GcmParams &p, int encrypt, int two_pass, int grid
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#endif  // ESPGPU_VARIANTS
+
 int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream,
                const GcmBsLaunch *bs) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1928,8 +1941,13 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
   if (!small) p.chunk = (GCM_WG / 64) * (64 / kGcmLanesPerRec);   // experiment: one pass per chunk
 #endif
   if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + p.chunk - 1) / p.chunk)));
+#ifdef ESPGPU_VARIANTS
   if (!small && p.ej0 != nullptr && bs != nullptr && bs->mode) return launch_gcm_bs(p, encrypt, two_pass, grid, st, *bs);
   if (!small && p.ej0 != nullptr) return launch_gcm_split(p, encrypt, two_pass, grid, st);
+#else
+  (void)bs;
+  if (!small && p.ej0 != nullptr) return -1;          // the split / bitsliced designs: variants build only
+#endif
   if (burst) {
     if (p.xin != nullptr && p.chunks != nullptr) return -1;   // self-staging: implicit chunks only
     if (p.xin != nullptr && encrypt)

@@ -79,8 +79,26 @@ struct Overflow {
   std::vector<uint8_t> bytes;
   std::vector<espgpu_seg> segpool;
   bool empty() const { return head == ent.size(); }
-  size_t footprint() const { return bytes.size() + (ent.size() - head) * sizeof(OvfEntry); }
+  // live bytes only: entries already moved into slots no longer count
+  size_t footprint() const {
+    return empty() ? 0 : bytes.size() - ent[head].pd.stage_off + (ent.size() - head) * sizeof(OvfEntry);
+  }
   void reset() { ent.clear(); head = 0; bytes.clear(); segpool.clear(); }
+  // drop the moved prefix (flush, once it is at least half the entries) so a
+  // sustained load that never empties the overflow does not grow it
+  void compact() {
+    if (empty()) { reset(); return; }
+    if (head < 64 || 2 * head < ent.size()) return;
+    const uint32_t b0 = ent[head].pd.stage_off, s0 = ent[head].pd.seg0;
+    bytes.erase(bytes.begin(), bytes.begin() + b0);
+    segpool.erase(segpool.begin(), segpool.begin() + s0);
+    ent.erase(ent.begin(), ent.begin() + (ptrdiff_t)head);
+    for (OvfEntry &e : ent) {
+      e.pd.stage_off -= b0;
+      e.pd.seg0 -= s0;
+    }
+    head = 0;
+  }
 };
 
 // Host memory registered with espgpu_register_host.
@@ -1081,7 +1099,7 @@ int espgpu_flush(espgpu_ctx *c) {
       o.head++;
     }
   }
-  if (o.empty() && !o.ent.empty()) o.reset();
+  if (!o.ent.empty()) o.compact();
   return 0;
 }
 
@@ -1287,7 +1305,7 @@ int espgpu_decrypt_batch_packed(espgpu_ctx *c, uint8_t *d_arena, const espgpu_de
                                 uint8_t *d_status, uint8_t *d_out, uint32_t out_stride, uint32_t flags,
                                 void *stream) {
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_out && n) || d_out == d_arena ||
-      out_stride == 0 || out_stride % 128 != 0)
+      out_stride == 0 || out_stride % 128 != 0 || ((uintptr_t)d_out & 127))
     return ESPGPU_EINVAL;
   return run_batch(c, d_arena, d_desc, n, d_status, d_out, flags, 0, reinterpret_cast<hipStream_t>(stream),
                    nullptr, 3, nullptr, out_stride);
@@ -1355,18 +1373,24 @@ int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_by
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
+  // the measured-slower designs exist only in the variants
+  // library (make -C f-stack_amd variants): ENOTSUP here for anything but
+  // the default
   if (!strcmp(key, "eta_fused")) {
     if (value < 0 || value > 3) return ESPGPU_EINVAL;
+    if (!kVariants && value != 2) return ESPGPU_ENOTSUP;
     c->eta_fused = value;
     return 0;
   }
   if (!strcmp(key, "gcm_split")) {
     if (value != 0 && value != 1) return ESPGPU_EINVAL;
+    if (!kVariants && value) return ESPGPU_ENOTSUP;
     c->gcm_split = value;
     return 0;
   }
   if (!strcmp(key, "gcm_bs")) {
     if (value < 0 || value > 2) return ESPGPU_EINVAL;
+    if (!kVariants && value) return ESPGPU_ENOTSUP;
     c->gcm_bs = value;
     return 0;
   }
@@ -1376,7 +1400,8 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
     return 0;
   }
   if (!strcmp(key, "overflow_mb")) {
-    if (value < 0 || value > 65536) return ESPGPU_EINVAL;
+    // offsets into the overflow's byte buffer are 32-bit (Pending::stage_off)
+    if (value < 0 || value > 4095) return ESPGPU_EINVAL;
     c->ovf_cap = (size_t)value << 20;
     // reserved up front: growing the overflow inside process() would copy it
     // (hundreds of microseconds at a few MiB)

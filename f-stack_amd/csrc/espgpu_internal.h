@@ -49,6 +49,13 @@ static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 //                      into LDS, the Horner multiplier, esp_gcm.hip gf_mul8).
 // [kGh8SmallOff, +64 KiB) the same for H^8: the Horner multiplier of the
 //                      small-batch kernel (kGcmLanesSmall lanes per record).
+// The measured-slower designs (GCM split / bitsliced, ETA MODE 0 / 5+6 / 7)
+// are compiled only into the variants library (-DESPGPU_VARIANTS).
+#ifdef ESPGPU_VARIANTS
+constexpr bool kVariants = true;
+#else
+constexpr bool kVariants = false;
+#endif
 constexpr int kGcmLanesPerRec = 4;                               // GCM kernel: lanes per record
 constexpr int kGcmLanesSmall = 8;                                // small batches: shorter serial chain
 constexpr uint32_t kGcmSmallBatch = 32768;                       // records: below, 8 lanes per record still fit the chip

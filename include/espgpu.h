@@ -251,11 +251,17 @@ int  espgpu_encrypt_batch(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu
 /* espgpu_decrypt_batch with a packed output: the plaintext (ESP payload) of
  * record i lands at d_out + i * out_stride instead of the record's own offset,
  * every 128-byte line of it written whole (out_stride a nonzero multiple of
- * 128; d_out != d_arena, n * out_stride bytes).  A record whose payload is
- * longer than out_stride is EINVAL.  For a device-side consumer of the
- * plaintext; the line-aligned stores make the kernel ≈ 6 % faster than the
- * record layout's.  GCM contexts only: ENOTSUP when the
- * context has ETA sessions.  No esp_input_cb trailer words. */
+ * 128; d_out 128-byte aligned, n * out_stride bytes, not overlapping d_arena:
+ * EINVAL for an unaligned d_out or d_out == d_arena; a partial overlap cannot
+ * be detected and races with the ciphertext reads).  A record whose payload
+ * is longer than out_stride is EINVAL.  Single pass, like the out-of-place
+ * espgpu_decrypt_batch: a record whose status is nonzero (EBADMSG) still has
+ * its unverified plaintext in its slot, which the consumer must ignore
+ * (swcr_gcm releases no plaintext for it, cryptosoft.c:600-603).  For a
+ * device-side consumer of the plaintext; the line-aligned stores make the
+ * kernel ≈ 4-6 % faster than the record layout's.  GCM
+ * contexts only: ENOTSUP when the context has ETA sessions.  No esp_input_cb
+ * trailer words. */
 int  espgpu_decrypt_batch_packed(espgpu_ctx *ctx, uint8_t *d_arena, const struct espgpu_desc *d_desc,
                                  uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t out_stride,
                                  uint32_t flags, void *stream);
@@ -353,7 +359,8 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *               (MODE 0), 0 separate verify / decrypt kernels, 3 verify and
  *               decrypt interleaved per wave out of place (MODE 7); others EINVAL;
  *   "overflow_mb" host overflow for process() while every staging slot is
- *               in flight, in MiB (0, the default: ERESTART; 0..65536);
+ *               in flight, in MiB (0, the default: ERESTART; 0..4095; only
+ *               requests not yet moved into a slot count against it);
  *   "xfer"      small batches' staging region moved by the xfer kernel (1,
  *               default) or by hipMemcpyAsync (0);
  *   "gcm_burst" GCM batches of up to this many records (default 4096) that

@@ -15,6 +15,15 @@ for p in (os.path.join(ROOT, "f-stack_amd"), os.path.join(ROOT, "oracle"), ROOT)
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# ESPGPU_VARIANTS=1: run the suite on libespgpu_variants.so, the engine plus
+# the measured-slower designs (GCM split / bitsliced passes, ETA MODE 0 /
+# 5+6 / 7), and add them to the parametrized GCM and ETA tests.
+# The default suite runs the shipped library's kernels only.
+VARIANTS = os.environ.get("ESPGPU_VARIANTS") == "1"
+if VARIANTS:
+    os.environ["ESPGPU_LIB"] = os.path.join(ROOT, "f-stack_amd", "libespgpu_variants.so")
+variants_only = pytest.mark.skipif(not VARIANTS, reason="variants library only (ESPGPU_VARIANTS=1)")
+
 
 def _make(args, fatal=True):
     try:
@@ -33,19 +42,26 @@ def pytest_configure(config):
     if os.path.isdir("/root/reference/freebsd"):
         _make(["-C", "oracle", "ref"], fatal=False)
     _make(["-C", "f-stack_amd", "-j8"])
+    if VARIANTS:
+        _make(["-C", "f-stack_amd", "-j8", "variants"])
 
 
-@pytest.fixture(params=[(4, 0, 0, 0), (8, 0, 0, 0), (4, 1, 0, 0), (8, 0, 1 << 30, 0), (4, 0, 0, 1), (4, 0, 0, 2)],
-                ids=["lanes4", "lanes8", "split", "burst", "bs", "bsconc"])
+_GCM_DESIGNS = [((4, 0, 0, 0), "lanes4"), ((8, 0, 0, 0), "lanes8"), ((8, 0, 1 << 30, 0), "burst")]
+if VARIANTS:
+    _GCM_DESIGNS += [((4, 1, 0, 0), "split"), ((4, 0, 0, 1), "bs"), ((4, 0, 0, 2), "bsconc")]
+
+
+@pytest.fixture(params=[d for d, _ in _GCM_DESIGNS], ids=[i for _, i in _GCM_DESIGNS])
 def gcm_lanes(request, drv):
-    """Run a GCM test through every GCM kernel design whatever its batch
-    size: the fused kernel with 4 lanes per record (throughput) and with 8
-    (small batches, half the serial steps), the split design (a CTR pass
-    then a GHASH / tag pass), the burst kernel (both passes in one launch;
-    decrypt in place keeps the fused kernel) and the bitsliced ctr pass with
-    the tag pass after it (bs) or, decrypting out of place, beside it on a
-    second stream (bsconc); set_tuning "gcm_lanes" / "gcm_split" /
-    "gcm_burst" / "gcm_bs", reset afterwards."""
+    """Run a GCM test through every shipped GCM kernel design whatever its
+    batch size: the fused kernel with 4 lanes per record (throughput) and
+    with 8 (small batches, half the serial steps), and the burst kernel (both
+    passes in one launch; decrypt in place keeps the fused kernel).  With
+    ESPGPU_VARIANTS=1 also the measured-slower designs: the split design (a
+    CTR pass then a GHASH / tag pass) and the bitsliced ctr pass with the tag
+    pass after it (bs) or, decrypting out of place, beside it on a second
+    stream (bsconc).  set_tuning "gcm_lanes" / "gcm_split" / "gcm_burst" /
+    "gcm_bs", reset afterwards."""
     lanes, split, burst, bs = request.param
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", lanes) == 0
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", split) == 0

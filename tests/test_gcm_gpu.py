@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import GcmSA, build_records, golden, oracle_decrypt
+from helpers import VARIANTS, GcmSA, build_records, golden, oracle_decrypt, variants_only
 
 pytestmark = pytest.mark.gpu
 
@@ -271,7 +271,7 @@ def test_invalid_records_einval(drv):
     drv.freesession(sids[0])
 
 
-@pytest.mark.parametrize("split", [0, 1], ids=["fused", "split"])
+@pytest.mark.parametrize("split", [0, pytest.param(1, marks=variants_only)], ids=["fused", "split"])
 def test_full_size_1m_x_1500_vs_oracle(drv, split):
     """cfg1 at full size (1M x 1500-B packets, one AES-128-GCM SA), every
     record against the oracle: GPU encrypt gives the oracle's arena byte for
@@ -672,26 +672,37 @@ def test_grouped_batch_sizes_across_the_small_batch_path(drv, n):
 
 def test_gcm_bs_knob_range(drv):
     """set_tuning "gcm_bs" takes 0, 1, 2 (the bitsliced CTR pass) and refuses
-    anything else with EINVAL, leaving the setting unchanged."""
+    anything else with EINVAL, leaving the setting unchanged; "gcm_split" 0
+    or 1.  The product library has neither design: ENOTSUP for anything but
+    0 (the variants library accepts them)."""
     for v in (-1, 3, 9):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 22
-    for v in (2, 1, 0):
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 0
+    for v in (2, 1):
+        assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == (0 if VARIANTS else 95)
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", 0) == 0
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 2) == 22
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 1) == (0 if VARIANTS else 95)
+    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0) == 0
 
 
-@pytest.mark.parametrize("lanes", [0, 4, 8])
+@pytest.mark.parametrize("lanes,burst", [(0, 4096), (4, 4096), (8, 4096), (0, 1 << 30)],
+                         ids=["auto", "lanes4", "lanes8", "burst"])
 @pytest.mark.parametrize("n,grouped", [(700, False), (40000, False), (40000, True)])
-def test_packed_output_vs_oracle(n, grouped, lanes):
+def test_packed_output_vs_oracle(n, grouped, lanes, burst):
     """espgpu_decrypt_batch_packed: record i's plaintext at out + i*stride
     (128-byte aligned), mixed sizes and sessions (planner) or one session
-    (caller-grouped), small (S = 8) and large batches; statuses and verified
-    plaintext vs the oracle, a record longer than the stride is EINVAL, the
-    bytes of each slot past its payload are never written."""
+    (caller-grouped), small (S = 8) and large batches, and with the burst
+    kernel enabled for every size (packed output always takes the fused
+    kernel); statuses and verified plaintext vs the oracle, a record longer
+    than the stride is EINVAL, the bytes of each slot past its payload are
+    never written.  A record that fails its tag (EBADMSG) holds its
+    unverified plaintext, as the header says: the consumer ignores it."""
     from espgpu.batch import decrypt_batch_packed
     from espgpu.opencrypto import GpuCryptoDriver
     d = GpuCryptoDriver(max_sessions=16)
     try:
         assert d.lib.espgpu_set_tuning(d.ctx, b"gcm_lanes", lanes) == 0      # 0: by batch size
+        assert d.lib.espgpu_set_tuning(d.ctx, b"gcm_burst", burst) == 0
         rng = np.random.default_rng(2100 + n + grouped)
         nsa = 1 if grouped else 3
         sas = [GcmSA(rng, klen=16 + 8 * (i % 3), mlen=(16, 12, 8)[i % 3]) for i in range(nsa)]
@@ -723,6 +734,12 @@ def test_packed_output_vs_oracle(n, grouped, lanes):
             assert (res[i, c:] == 0xA5).all(), i
         for i in np.flatnonzero(cts > stride):
             assert (res[i] == 0xA5).all(), i
+        # only the ICV was flipped: the unverified plaintext is the true one
+        for i in np.flatnonzero(got == O.EBADMSG):
+            o, L, ml = int(descs["off4"][i]) * 4, int(descs["len"][i]), sas[sa_idx[i]].mlen
+            c = L - 16 - ml
+            assert res[i, :c].tobytes() == plain[o + 16:o + 16 + c].tobytes(), i
+        assert (got == O.EBADMSG).sum() > 0
         for s in sids:
             d.freesession(s)
     finally:
@@ -730,8 +747,8 @@ def test_packed_output_vs_oracle(n, grouped, lanes):
 
 
 def test_packed_output_rejects(drv):
-    """Stride not a multiple of 128, in place, or a context holding ETA
-    sessions: EINVAL / ENOTSUP."""
+    """Stride not a multiple of 128, in place, an unaligned output, or a
+    context holding ETA sessions: EINVAL / ENOTSUP."""
     from espgpu.esp import CBC_SHA1, SecAssoc
     z = torch.zeros(4096, dtype=torch.uint8, device="cuda")
     dsc = torch.zeros(16, dtype=torch.uint8, device="cuda")
@@ -744,6 +761,9 @@ def test_packed_output_rejects(drv):
                                          1500, 0, None) == 22
     assert L.espgpu_decrypt_batch_packed(drv.ctx, z.data_ptr(), dsc.data_ptr(), 1, st.data_ptr(), out.data_ptr(),
                                          0, 0, None) == 22
+    # d_out not 128-byte aligned
+    assert L.espgpu_decrypt_batch_packed(drv.ctx, z.data_ptr(), dsc.data_ptr(), 1, st.data_ptr(),
+                                         out.data_ptr() + 64, 1536, 0, None) == 22
     rc, sid = drv.newsession(SecAssoc(0x4242, CBC_SHA1, bytes(16), bytes(20)).csp())
     assert rc == 0
     try:

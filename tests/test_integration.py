@@ -37,6 +37,18 @@ def test_kernel_driver_errno_and_erestart():
     assert "kmock cpu OK" in r.stdout
 
 
+def test_kernel_driver_python_harness_builds():
+    """integration/libkmockdrv.so (ff_gpucrypto.c over kmock + the host shim,
+    flat entry points for tests/test_kmock_driver_gpu.py) builds, loads and
+    exports them (no compute calls: no GPU here)."""
+    import ctypes
+    _make()
+    L = ctypes.CDLL(os.path.join(D, "libkmockdrv.so"))
+    for s in ("kd_open", "kd_close", "kd_newsession", "kd_freesession", "kd_request", "kd_dispatch",
+              "kd_poll", "kd_result", "kd_free", "kd_register", "kd_counters", "kd_engine"):
+        assert hasattr(L, s), s
+
+
 @pytest.mark.gpu
 def test_kernel_driver_on_gpu():
     exe = os.path.join(D, "kmock_gpu_test")

@@ -241,6 +241,59 @@ def test_overflow_keeps_accepting_while_slots_in_flight():
             assert crps[i].crp_etype == 0
             assert bytes(pkts[i][16:L - 16]) == bytes(plain[o + 16:o + L - 16])
         assert drv.set_tuning("overflow_mb", -1) == 22
+        # overflow offsets are 32-bit: past 4095 MiB the setting is refused
+        assert drv.set_tuning("overflow_mb", 4096) == 22
+        assert drv.set_tuning("overflow_mb", 4095) == 0
+    finally:
+        drv.close()
+
+
+def test_overflow_sustained_load_stays_within_cap():
+    """A backlog that never drains: 200 requests wait in a 1-MiB overflow,
+    then 4 arrive per main_loop iteration while 4 complete, for 2000 more
+    (≈ 3 MB through an overflow that is never empty).  Only live requests
+    count against the cap, so no request is refused (ERESTART), and every
+    one completes bit-exact in arrival order."""
+    from espgpu.esp import esp_input_crp
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=4, batch_records=4, nbatches=2)
+    try:
+        assert drv.set_tuning("overflow_mb", 1) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2350)
+        m = 64                                             # distinct records, reused
+        sas, idx, plain, ct, descs = _gcm_reqs(rng, m, 1448)
+        ses = [fw.crypto_newsession(s.esp_sa().csp())[1] for s in sas]
+        n, pre = 2200, 200
+        pkts, crps = [], []
+        for i in range(n):
+            k = i % m
+            o, L = int(descs["off4"][k]) * 4, int(descs["len"][k])
+            pkts.append(bytearray(bytes(ct[o:o + L])))
+            crps.append(esp_input_crp(fw, ses[idx[k]], sas[idx[k]].esp_sa(), pkts[i], 0))
+        s0 = drv.stats()
+        order = []
+        for i in range(pre):
+            assert drv.process(crps[i]) == 0
+        for i in range(pre, n, 4):
+            for c in crps[i:i + 4]:
+                assert drv.process(c) == 0                 # never ERESTART
+            want, spins = len(order) + 4, 0
+            while len(order) < want:
+                drv.flush()
+                order += [id(c) for c in drv.poll()]
+                spins += 1
+                assert spins < 10**6
+        while len(order) < n:
+            drv.flush()
+            order += [id(c) for c in drv.poll()]
+        assert drv.stats()["erestart"] == s0["erestart"]
+        assert order == [id(c) for c in crps]
+        for i in range(n):
+            k = i % m
+            o, L = int(descs["off4"][k]) * 4, int(descs["len"][k])
+            assert crps[i].crp_etype == 0
+            assert bytes(pkts[i][16:L - 16]) == bytes(plain[o + 16:o + L - 16])
     finally:
         drv.close()
 
