@@ -102,6 +102,9 @@ ff_nexus_add_driver(driver_t *drv)
 	struct device *d;
 	int error;
 
+	/* the static DEVICE_IDENTIFY looks up drv->ops: compile the class first,
+	 * as devclass_add_driver does (subr_bus.c) */
+	kobj_class_compile((kobj_class_t)drv);
 	DEVICE_IDENTIFY(drv, &ff_nexus);
 	for (d = ff_nexus.next; d != NULL; d = d->next) {
 		if (d->attached || strcmp(d->name, drv->name) != 0)

@@ -117,34 +117,43 @@ def c_definitions(text):
     return names
 
 
+def build_kernel(ref, work, jobs, extra_make=""):
+    """Copy + patch the F-Stack tree into `work` and compile every kernel-domain
+    object with lib/Makefile's own rules.  -> (lib dir, make argv, objects,
+    report, make's return code)"""
+    if os.path.isdir(work):
+        shutil.rmtree(work)
+    os.makedirs(work)
+    for d in ("lib", "mk"):
+        shutil.copytree(os.path.join(ref, d), os.path.join(work, d), symlinks=True)
+    os.symlink(os.path.join(ref, "freebsd"), os.path.join(work, "freebsd"))
+    run(["sh", os.path.join(HERE, "apply_fstack.sh"), work])
+    lib = os.path.join(work, "lib")
+    mk = os.path.join(lib, "Makefile")
+    text = open(mk).read()
+    guard = re.search(r"ifneq \(\$\(shell pkg-config --exists libdpdk && echo 0\),0\)\n.*\nendif\n", text)
+    assert guard, "lib/Makefile's DPDK guard not found"
+    open(mk, "w").write(text.replace(guard.group(0), "# (DPDK guard dropped: kernel-domain check)\n"))
+    open(os.path.join(work, "vars.mk"), "w").write(MAKEVARS + extra_make)
+    make = ["make", "-s", "-f", "Makefile", "-f", "../vars.mk", "FF_IPSEC=1", "FF_IPSEC_GPU=1",
+            "ESPGPU_ROOT=" + os.path.dirname(HERE)]
+    run(make + ["kgen"], cwd=lib)
+    r = run(make + ["-k", f"-j{jobs}", "kobjs"], cwd=lib, check=False)
+    errors = [l for l in (r.stdout + r.stderr).splitlines() if "error" in l]
+    objs = run(make + ["print-objs"], cwd=lib).stdout.split()
+    report = {"kernel_objects": len(objs), "compile_errors": errors}
+    return lib, make, objs, report, r.returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--work", default="/tmp/fstack_build_check")
     ap.add_argument("-j", type=int, default=8)
     a = ap.parse_args()
-    if os.path.isdir(a.work):
-        shutil.rmtree(a.work)
-    os.makedirs(a.work)
-    for d in ("lib", "mk"):
-        shutil.copytree(os.path.join(a.ref, d), os.path.join(a.work, d), symlinks=True)
-    os.symlink(os.path.join(a.ref, "freebsd"), os.path.join(a.work, "freebsd"))
-    run(["sh", os.path.join(HERE, "apply_fstack.sh"), a.work])
-    lib = os.path.join(a.work, "lib")
-    mk = os.path.join(lib, "Makefile")
-    text = open(mk).read()
-    guard = re.search(r"ifneq \(\$\(shell pkg-config --exists libdpdk && echo 0\),0\)\n.*\nendif\n", text)
-    assert guard, "lib/Makefile's DPDK guard not found"
-    open(mk, "w").write(text.replace(guard.group(0), "# (DPDK guard dropped: kernel-domain check)\n"))
-    open(os.path.join(a.work, "vars.mk"), "w").write(MAKEVARS)
-    make = ["make", "-s", "-f", "Makefile", "-f", "../vars.mk", "FF_IPSEC=1", "FF_IPSEC_GPU=1",
-            "ESPGPU_ROOT=" + os.path.dirname(HERE)]
-    run(make + ["kgen"], cwd=lib)
-    r = run(make + ["-k", f"-j{a.j}", "kobjs"], cwd=lib, check=False)
-    errors = [l for l in (r.stdout + r.stderr).splitlines() if "error" in l]
-    objs = run(make + ["print-objs"], cwd=lib).stdout.split()
-    report = {"kernel_objects": len(objs), "compile_errors": errors}
-    if r.returncode != 0:
+    lib, make, objs, report, rc = build_kernel(a.ref, a.work, a.j)
+    errors = report["compile_errors"]
+    if rc != 0:
         report["unresolved"] = ["<kernel-domain compile failed>"]
         print(json.dumps(report, indent=1))
         return 1
