@@ -13,7 +13,10 @@ coalesced read (16 B/lane loads), so it is doubled; WRITE_SIZE is exact for
   lds_frac  = SQ_LDS_IDX_ACTIVE / 256 CUs / kernel cycles   (LDS-array busy share)
   valu_frac = SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / kernel cycles (a wave64 VALU
               instruction holds its SIMD 2 cycles on gfx950, MI355X_MICROARCH.md:54)
-and the floor each resource alone would set at that clock.
+and the floor each resource alone would set at that clock.  GRBM_GUI_ACTIVE
+counts the whole counter window, not only the kernel, so for short launches it
+implies a clock above the chip's 2.4 GHz: `pipes` is omitted (with the reason)
+for kernels under 0.1 ms or whenever the implied clock exceeds 2.4 GHz.
 """
 import collections
 import csv
@@ -22,6 +25,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MAX_CLOCK_GHZ = 2.4          # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def kernel_stats(d):
@@ -59,6 +63,9 @@ def pipes(c, kern_ms):
     """Busy shares of the LDS array and the VALU issue slots (module docstring)."""
     cyc = c["GRBM_GUI_ACTIVE"] / 8
     ghz = cyc / (kern_ms * 1e6)
+    if kern_ms < 0.1 or ghz > MAX_CLOCK_GHZ:
+        return {"omitted": "kernel %.4f ms, implied clock %.2f GHz: the counter window is not the kernel"
+                           % (kern_ms, ghz)}
     out = {"kernel_cycles": round(cyc), "clock_ghz": round(ghz, 3)}
     if "SQ_LDS_IDX_ACTIVE" in c:
         lds = c["SQ_LDS_IDX_ACTIVE"] / 256
