@@ -1455,24 +1455,156 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
 // ciphertext it wrote (ICV, status).
 // STAGE: the batch stages its own records (stage_in / the epilogue, as
 // gcm_kernel<..., true>): one launch per burst.
-template <int DIR, int WG, bool STAGE = false>
-__global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
+// The per-session state a burst workgroup keeps across chunks (the H^8
+// table in LDS belongs to cur_sa).
+struct BurstSA {
+  uint32_t cur = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
+};
+
+// One chunk of the burst design (gcm_burst_kernel; gcm_door_kernel runs the
+// same body per claimed chunk): records [start, start + count) of p, session
+// `sa` (~0u: the chunk's first descriptor's, read after staging).  `first`
+// only gates the phase clock.
+template <int DIR, int WG, bool STAGE>
+__device__ __forceinline__ void burst_chunk(const GcmParams &p, uint8_t *lds, uint32_t start, uint32_t count,
+                                            uint32_t sa, BurstSA &ss, uint4 *s_z, XferSpan *s_xout, bool first) {
   constexpr int ST = kGcmLanesSmall;
   [[maybe_unused]] constexpr int S = ST;    // for the phase clock
-  GCM_PHASE(0, true);
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < 256 * 32; idx += WG) {
+  const int wave = tid >> 6;
+  if (STAGE) stage_in<WG>(p, start, count, s_xout);
+  if (sa == 0xffffffffu) sa = p.desc[start].sa;
+  sa = __builtin_amdgcn_readfirstlane(sa);
+  if (sa != ss.cur) {
+    __syncthreads();
+    if (sa < p.nsas) {
+      const DevSA *s = p.sas + sa;
+      ss.nr = s->nr;
+      ss.flags = s->flags;
+      ss.mlen = s->mlen;
+      ss.mode = s->mode;
+      if (ss.mode == ESPGPU_CSP_MODE_AEAD) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + kGh8SmallOff);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
+#pragma unroll 4
+        for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+      }
+    } else {
+      ss.mode = 0;
+    }
+    ss.cur = sa;
+    __syncthreads();
+  }
+  const uint32_t nr = ss.nr, flags = ss.flags, mlen = ss.mlen;
+  if (ss.mode != ESPGPU_CSP_MODE_AEAD) {
+    // as gcm_kernel: EINVAL unless the ETA kernel's record
+    for (uint32_t r = (uint32_t)tid; r < count; r += WG) {
+      const uint32_t pos = start + r;
+      const uint32_t di = p.order ? p.order[pos] : pos;
+      const uint32_t rsa = p.desc[di].sa;
+      const bool eta = rsa < p.nsas && p.sas[rsa].mode == ESPGPU_CSP_MODE_ETA;
+      if (!eta) {
+        p.status[di] = ESPGPU_EINVAL;
+        if (DIR == 0 && p.trailer) p.trailer[di] = 0;
+      }
+    }
+    if (STAGE) {
+      // the statuses go back to the host (no results: nothing verified)
+      __syncthreads();
+      for (uint32_t r = (uint32_t)tid; r < count; r += WG) p.hstat[start + r] = p.status[start + r];
+    }
+    return;
+  }
+  GCM_PHASE(3, first);
+  const rkptr rk = (rkptr)(const void *)(p.sas[sa].rk);
+  constexpr uint32_t kCtrRpw = 64 / kBurstCtrLanes, kTagRpw = 64 / ST;
+  if (DIR == 0) {
+    constexpr uint32_t kCw = kBurstCtrWaves, kTw = WG / 64 - kBurstCtrWaves;
+    if ((uint32_t)wave < kCw) {
+      for (uint32_t sub = 0; sub < count; sub += kCw * kCtrRpw) {
+        const uint32_t rl = sub + (uint32_t)wave * kCtrRpw + (uint32_t)((tid & 63) / kBurstCtrLanes);
+        const bool have = rl < count;
+        const uint32_t pos = start + (have ? rl : 0);
+        const uint32_t di = p.order ? p.order[pos] : pos;
+        if (__any(have)) ctr_group<0, kBurstCtrLanes, true>(p, lds, di, have, sa, mlen, (int)nr, rk, LDS_TP);
+      }
+    } else {
+      for (uint32_t sub = 0; sub < count; sub += kTw * kTagRpw) {
+        const uint32_t rl = sub + ((uint32_t)wave - kCw) * kTagRpw + (uint32_t)((tid & 63) / ST);
+        const bool have = rl < count;
+        const uint32_t pos = start + (have ? rl : 0);
+        const uint32_t di = p.order ? p.order[pos] : pos;
+        if (__any(have)) tag_group<0, ST>(p, lds, di, have, sa, flags, mlen, s_z, rl);
+      }
+    }
+    GCM_PHASE(4, first);
+    __syncthreads();
+    GCM_PHASE(5, first);
+    for (uint32_t r = (uint32_t)tid; r < count; r += WG) {
+      const uint32_t pos = start + r;
+      tag_finish(p, p.order ? p.order[pos] : pos, sa, mlen, s_z[r]);
+    }
+    // s_z is rewritten by the next chunk's hash waves
+    __syncthreads();
+  } else {
+    for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * kCtrRpw) {
+      const uint32_t rl = sub + (uint32_t)wave * kCtrRpw + (uint32_t)((tid & 63) / kBurstCtrLanes);
+      const bool have = rl < count;
+      const uint32_t pos = start + (have ? rl : 0);
+      const uint32_t di = p.order ? p.order[pos] : pos;
+      if (__any(have)) ctr_group<1, kBurstCtrLanes, true>(p, lds, di, have, sa, mlen, (int)nr, rk, LDS_TP);
+    }
+    // the ciphertext and E_K(J0) written above are read below by other waves
+    __syncthreads();
+    for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * kTagRpw) {
+      const uint32_t rl = sub + (uint32_t)wave * kTagRpw + (uint32_t)((tid & 63) / ST);
+      const bool have = rl < count;
+      const uint32_t pos = start + (have ? rl : 0);
+      const uint32_t di = p.order ? p.order[pos] : pos;
+      if (__any(have)) tag_group<1, ST>(p, lds, di, have, sa, flags, mlen);
+    }
+  }
+  if (STAGE) {
+    // statuses and the results of the records that passed back to the host
+    __syncthreads();
+    for (uint32_t r = (uint32_t)wave; r < count; r += (uint32_t)(WG / 64)) {
+      const uint32_t di = start + r;
+      const uint8_t st = p.status[di];
+      if ((tid & 63) == 0) p.hstat[di] = st;
+      if (st == ESPGPU_OK) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const XferSpan sp = s_xout[2 * r + k];
+          if (sp.len) xfer_copy(sp.src, sp.dst, sp.len, (uint32_t)(tid & 63), 64u);
+        }
+      }
+    }
+  }
+  GCM_PHASE(6, first);
+}
+
+// The T-table pair into LDS (entry x: 32 slots of Te0, then 32 of Te1; tpa()).
+template <int WG>
+__device__ __forceinline__ void load_tpair(uint8_t *lds, const uint2 *tpair) {
+  for (int idx = threadIdx.x; idx < 256 * 32; idx += WG) {
     const int x = idx >> 5, r = idx & 31;
-    const uint2 t = p.tpair[x];
+    const uint2 t = tpair[x];
     *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
     *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
   }
+}
+
+template <int DIR, int WG, bool STAGE = false>
+__global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
+  [[maybe_unused]] constexpr int S = kGcmLanesSmall;    // for the phase clock
+  GCM_PHASE(0, true);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const int tid = threadIdx.x;
+  load_tpair<WG>(lds, p.tpair);
   GCM_PHASE(1, true);
   const bool implicit = (p.chunks == nullptr);
   const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
-  uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
-  const int wave = tid >> 6;
+  BurstSA ss;
   __shared__ uint4 s_z[DIR == 0 ? kChunkRecs : 1];
   __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
   __shared__ uint32_t s_ticket[2];
@@ -1482,124 +1614,159 @@ __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
     const uint32_t c = s_ticket[it & 1];
     GCM_PHASE(2, it == 0);
     if (c >= nch) break;
-    uint32_t sa, start, count;
     if (implicit) {
-      start = c * p.chunk;
-      count = min(p.chunk, p.n - start);
-      if (STAGE) stage_in<WG>(p, start, count, s_xout);
-      sa = p.desc[start].sa;
+      const uint32_t start = c * p.chunk;
+      burst_chunk<DIR, WG, STAGE>(p, lds, start, min(p.chunk, p.n - start), 0xffffffffu, ss, s_z, s_xout, it == 0);
     } else {
       const Chunk ch = p.chunks[c];
-      sa = ch.sa;
-      start = ch.start;
-      count = ch.count;
+      burst_chunk<DIR, WG, STAGE>(p, lds, ch.start, ch.count, ch.sa, ss, s_z, s_xout, it == 0);
     }
-    sa = __builtin_amdgcn_readfirstlane(sa);
-    if (sa != cur_sa) {
-      __syncthreads();
-      if (sa < p.nsas) {
-        const DevSA *s = p.sas + sa;
-        nr = s->nr;
-        flags = s->flags;
-        mlen = s->mlen;
-        mode = s->mode;
-        if (mode == ESPGPU_CSP_MODE_AEAD) {
-          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + kGh8SmallOff);
-          uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
-#pragma unroll 4
-          for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
-        }
-      } else {
-        mode = 0;
-      }
-      cur_sa = sa;
-      __syncthreads();
-    }
-    if (mode != ESPGPU_CSP_MODE_AEAD) {
-      // as gcm_kernel: EINVAL unless the ETA kernel's record
-      for (uint32_t r = (uint32_t)tid; r < count; r += WG) {
-        const uint32_t pos = start + r;
-        const uint32_t di = p.order ? p.order[pos] : pos;
-        const uint32_t rsa = p.desc[di].sa;
-        const bool eta = rsa < p.nsas && p.sas[rsa].mode == ESPGPU_CSP_MODE_ETA;
-        if (!eta) {
-          p.status[di] = ESPGPU_EINVAL;
-          if (DIR == 0 && p.trailer) p.trailer[di] = 0;
-        }
-      }
-      continue;
-    }
-    GCM_PHASE(3, it == 0);
-    const rkptr rk = (rkptr)(const void *)(p.sas[sa].rk);
-    constexpr uint32_t kCtrRpw = 64 / kBurstCtrLanes, kTagRpw = 64 / ST;
-    if (DIR == 0) {
-      constexpr uint32_t kCw = kBurstCtrWaves, kTw = WG / 64 - kBurstCtrWaves;
-      if ((uint32_t)wave < kCw) {
-        for (uint32_t sub = 0; sub < count; sub += kCw * kCtrRpw) {
-          const uint32_t rl = sub + (uint32_t)wave * kCtrRpw + (uint32_t)((tid & 63) / kBurstCtrLanes);
-          const bool have = rl < count;
-          const uint32_t pos = start + (have ? rl : 0);
-          const uint32_t di = p.order ? p.order[pos] : pos;
-          if (__any(have)) ctr_group<0, kBurstCtrLanes, true>(p, lds, di, have, sa, mlen, (int)nr, rk, LDS_TP);
-        }
-      } else {
-        for (uint32_t sub = 0; sub < count; sub += kTw * kTagRpw) {
-          const uint32_t rl = sub + ((uint32_t)wave - kCw) * kTagRpw + (uint32_t)((tid & 63) / ST);
-          const bool have = rl < count;
-          const uint32_t pos = start + (have ? rl : 0);
-          const uint32_t di = p.order ? p.order[pos] : pos;
-          if (__any(have)) tag_group<0, ST>(p, lds, di, have, sa, flags, mlen, s_z, rl);
-        }
-      }
-      GCM_PHASE(4, it == 0);
-      __syncthreads();
-      GCM_PHASE(5, it == 0);
-      for (uint32_t r = (uint32_t)tid; r < count; r += WG) {
-        const uint32_t pos = start + r;
-        tag_finish(p, p.order ? p.order[pos] : pos, sa, mlen, s_z[r]);
-      }
-      // s_z is rewritten by the next chunk's hash waves
-      __syncthreads();
-    } else {
-      for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * kCtrRpw) {
-        const uint32_t rl = sub + (uint32_t)wave * kCtrRpw + (uint32_t)((tid & 63) / kBurstCtrLanes);
-        const bool have = rl < count;
-        const uint32_t pos = start + (have ? rl : 0);
-        const uint32_t di = p.order ? p.order[pos] : pos;
-        if (__any(have)) ctr_group<1, kBurstCtrLanes, true>(p, lds, di, have, sa, mlen, (int)nr, rk, LDS_TP);
-      }
-      // the ciphertext and E_K(J0) written above are read below by other waves
-      __syncthreads();
-      for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * kTagRpw) {
-        const uint32_t rl = sub + (uint32_t)wave * kTagRpw + (uint32_t)((tid & 63) / ST);
-        const bool have = rl < count;
-        const uint32_t pos = start + (have ? rl : 0);
-        const uint32_t di = p.order ? p.order[pos] : pos;
-        if (__any(have)) tag_group<1, ST>(p, lds, di, have, sa, flags, mlen);
-      }
-    }
-    if (STAGE) {
-      // statuses and the results of the records that passed back to the host
-      __syncthreads();
-      for (uint32_t r = (uint32_t)wave; r < count; r += (uint32_t)(WG / 64)) {
-        const uint32_t di = start + r;
-        const uint8_t st = p.status[di];
-        if ((tid & 63) == 0) p.hstat[di] = st;
-        if (st == ESPGPU_OK) {
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const XferSpan sp = s_xout[2 * r + k];
-            if (sp.len) xfer_copy(sp.src, sp.dst, sp.len, (uint32_t)(tid & 63), 64u);
-          }
-        }
-      }
-    }
-    GCM_PHASE(6, it == 0);
   }
   GCM_PHASE(7, true);
   if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
     atomicExch(&p.queue[0], 0u);
     atomicExch(&p.queue[1], 0u);
+  }
+}
+
+// ---- doorbell kernel: the burst kernel as a persistent service -------------
+// (espgpu_internal.h DoorCtl / DoorDev; set_tuning "door").  What a launched
+// burst pays besides its crypto (phase clock, 32 registered records: 40 us
+// per burst, 21 us of it in the kernel) is the launch and completion
+// signalling and, inside the kernel, the T-table and H^8-table fills (3 us)
+// and a cold ticket atomic.  Here the workgroups stay resident with both
+// tables in LDS: thread 0 polls the job ring in host memory (one 16-byte
+// read per poll over PCIe), claims chunk (job, c) with a CAS on the device
+// claim counter, and the workgroup runs burst_chunk on it, staging records in
+// from and results out to host memory as the launched burst kernel does.
+// Every wave reaches the exit: stop set by the host, or idle_ticks without a
+// claim (poll() relaunches the kernel for a job published after that).
+template <int WG>
+__global__ __launch_bounds__(WG) void gcm_door_kernel(DoorArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  __shared__ uint4 s_z[kChunkRecs];
+  __shared__ XferSpan s_xout[2 * kChunkRecs];
+  __shared__ uint32_t s_cmd[2][4];                 // job, chunk, n, slot_op (double-buffered by parity)
+  const int tid = threadIdx.x;
+  load_tpair<WG>(lds, a.tpair);
+  BurstSA ss;
+  constexpr uint32_t kExit = 0xffffffffu;
+  // thread 0's view of the ring: the job it claims in, and that job's entry
+  uint32_t cur = 0, en = 0, eso = 0, enc = 0;
+  bool have = false;
+  for (uint32_t it = 0;; ++it) {
+    uint32_t *cmd = s_cmd[it & 1];
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t job = kExit, c = 0, n = 0, so = 0;
+      typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+      for (uint32_t poll = 0;; ++poll) {
+        // (stop is read on every 4th poll: each read is a PCIe round trip)
+        if ((poll & 3) == 0 && *reinterpret_cast<volatile uint32_t *>(&a.ctl->stop)) break;
+        if (!have) {
+          const uint32_t hint = __hip_atomic_load(&a.dev->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((int32_t)(hint - cur) > 0) cur = hint;
+          const V4 e = *reinterpret_cast<const volatile V4 *>(&a.ctl->ring[cur % kDoorRing]);   // one 16-byte read
+          if (e.w == cur + 1 && e.z == (e.x ^ e.y ^ e.w ^ kDoorChk)) {
+            have = true;
+            en = e.x, eso = e.y, enc = (e.x + a.chunk - 1) / a.chunk;
+          } else if ((int32_t)(e.w - (cur + 1)) > 0) {
+            ++cur;                         // the entry holds a later job: job cur is long done
+            continue;
+          } else {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.idle_ticks) break;
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+          }
+        }
+        unsigned long long *tw = &a.dev->tick[cur % kDoorRing];
+        const unsigned long long w = __hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int32_t)((uint32_t)(w >> 32) - (cur + 1)) < 0) {
+          // install job cur's generation (it is published: this thread saw it)
+          unsigned long long exp = w;
+          __hip_atomic_compare_exchange_strong(tw, &exp, (unsigned long long)(cur + 1) << 32, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          continue;
+        }
+        const unsigned long long t = __hip_atomic_fetch_add(tw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t g = (uint32_t)(t >> 32), cc = (uint32_t)t;
+        if (g == cur + 1) {
+          if (cc < enc) {
+            job = cur, c = cc, n = en, so = eso;
+            break;
+          }
+          // every chunk of job cur is claimed: on to the next job
+          __hip_atomic_fetch_max(&a.dev->next, cur + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ++cur;
+          have = false;
+          continue;
+        }
+        // the add landed on a later job's generation (g - 1, published when
+        // it was installed): chunk cc of that job is this workgroup's unless
+        // the job already had all its chunks claimed
+        const uint32_t jj = g - 1;
+        const V4 e = *reinterpret_cast<const volatile V4 *>(&a.ctl->ring[jj % kDoorRing]);
+        cur = jj;
+        have = false;
+        if (e.w == jj + 1 && e.z == (e.x ^ e.y ^ e.w ^ kDoorChk)) {
+          have = true;
+          en = e.x, eso = e.y, enc = (e.x + a.chunk - 1) / a.chunk;
+          if (cc < enc) {
+            job = jj, c = cc, n = en, so = eso;
+            break;
+          }
+        }
+      }
+      // the job's host data (descriptors, spans, records) as published: no
+      // line cached from an earlier job at the same addresses survives
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      cmd[0] = job;
+      cmd[1] = c;
+      cmd[2] = n;
+      cmd[3] = so;
+    }
+    __syncthreads();
+    const uint32_t job = cmd[0];
+    if (job == kExit) break;
+    const uint32_t c = cmd[1], n = cmd[2], slot = cmd[3] & 0xffffu, op = cmd[3] >> 16;
+    if (slot < a.nslots) {
+      const DoorSlot sl = a.slots[slot];
+      GcmParams p{};
+      uint8_t *res = op ? sl.arena : sl.out;
+      p.arena = sl.arena;
+      p.out = res;
+      p.desc = reinterpret_cast<const espgpu_desc *>(sl.arena + sl.desc_off);
+      p.n = n;
+      p.sas = a.sas;
+      p.gtab = a.gtab;
+      p.tpair = a.tpair;
+      p.status = res + sl.stat_off;
+      p.nsas = a.nsas;
+      p.chunk = a.chunk;
+      p.ej0 = sl.ej0;
+      p.xin = sl.xin;
+      p.xout = sl.xout;
+      p.hstat = sl.hstat;
+      p.hdesc = reinterpret_cast<const espgpu_desc *>(sl.hdesc);
+      const uint32_t start = c * a.chunk, count = min(a.chunk, n - start);
+      if (op)
+        burst_chunk<1, WG, true>(p, lds, start, count, 0xffffffffu, ss, s_z, s_xout, false);
+      else
+        burst_chunk<0, WG, true>(p, lds, start, count, 0xffffffffu, ss, s_z, s_xout, false);
+    }
+    // every wave's host writes (results, statuses) complete and visible
+    // before the job can be signalled done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t nch = (n + a.chunk - 1) / a.chunk;
+      const uint32_t f = __hip_atomic_fetch_add(&a.dev->fin[job % kDoorRing], 1u, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      if (f == nch - 1) {
+        __hip_atomic_store(&a.dev->fin[job % kDoorRing], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.ctl->done[job % kDoorRing], job + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -1913,6 +2080,12 @@ static int launch_gcm_bs(const GcmParams &p, int encrypt, int two_pass, int grid
 }
 
 #endif  // ESPGPU_VARIANTS
+
+int launch_gcm_door(const DoorArgs &a, int grid, void *stream) {
+  hipLaunchKernelGGL((gcm_door_kernel<kBurstWG>), dim3(grid), dim3(kBurstWG), 0,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream,
                const GcmBsLaunch *bs) {

@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <string>
@@ -137,6 +138,12 @@ struct Slot {
   hipEvent_t in_done = nullptr, k0 = nullptr, k1 = nullptr, kout = nullptr, done = nullptr;
   bool timed = false;                       // k0 / k1 recorded around the kernels
   hipStream_t st = nullptr;                 // small batches: copy, kernel, copy in order here
+  // doorbell path (set_tuning "door"): the job number this slot's batch was
+  // published as (-1: launched, or free), when, and its own E_K(J0) scratch
+  // (jobs of different slots run at once)
+  int64_t door_job = -1;
+  uint64_t door_t0 = 0;
+  uint4 *d_ej0 = nullptr;
 };
 
 }  // namespace
@@ -201,6 +208,19 @@ struct espgpu_ctx {
   int xfer_small = 1;            // small batches: staging region moved by the xfer kernel (else hipMemcpyAsync)
   int stage_fused = 1;           // small single-session GCM batches stage their own records (one launch)
   uint32_t gcm_burst = GCM_BURST_DEFAULT;   // small GCM batches of <= this many records: burst kernel
+  // doorbell burst path (set_tuning "door", espgpu_internal.h DoorCtl): a
+  // persistent kernel of door_wg workgroups serves single-session GCM
+  // batches of <= gcm_burst records with no launch per batch
+  int door_wg = 0;
+  uint32_t door_idle_us = 20000;             // the kernel exits after this long without a job
+  DoorCtl *door_ctl = nullptr, *door_ctl_dev = nullptr;
+  DoorDev *d_door = nullptr;
+  DoorSlot *d_door_slots = nullptr;
+  hipStream_t s_door = nullptr;
+  hipEvent_t ev_door = nullptr;
+  bool door_live = false;                    // launched and not seen to have exited
+  uint32_t door_next = 0;                    // next job number
+  uint64_t door_last_pub = 0;                // host clock (ns) of the last publish
   std::vector<HostRegion> regions;   // sorted by base
   // completions not yet handed to poll(): ready[ready_head..] (host-side
   // rejects and finished batches), reserved so steady state does not allocate
@@ -315,6 +335,7 @@ void free_slot(Slot &s) {
   if (s.st) hipStreamSynchronize(s.st);
   hipHostFree(s.h_arena);
   hipHostFree(s.h_xfer);
+  hipFree(s.d_ej0);
   delete[] s.h_desc;
   hipFree(s.d_arena); hipFree(s.d_out);
   for (hipEvent_t e : {s.done, s.in_done, s.k0, s.k1, s.kout})
@@ -375,6 +396,135 @@ void slot_commit(Slot &s, Pending pd, espgpu_desc d, const espgpu_seg *segs, int
 bool slot_full(const espgpu_ctx *c, const Slot &s, int op, uint32_t rlen) {
   return s.state == SLOT_FILLING &&
          (s.op != op || s.nrec >= c->cfg.batch_records || s.bytes + rlen + 16 > c->cfg.batch_bytes);
+}
+
+uint64_t now_ns() {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+// ---- doorbell burst path (espgpu_internal.h DoorCtl) -------------------------
+// A door batch's descriptors and statuses sit at fixed offsets of its slot
+// (after the largest record region), so the device slot table never changes
+// per batch; its xout spans start at h_xfer + batch_records.
+uint32_t door_desc_off(const espgpu_ctx *c) { return c->cfg.batch_bytes + 16; }
+uint32_t door_stat_off(const espgpu_ctx *c) { return door_desc_off(c) + c->cfg.batch_records * (uint32_t)sizeof(espgpu_desc); }
+constexpr uint32_t kDoorChunk = 4;           // records per claimed chunk (the burst kernel's)
+
+int door_write_slot(espgpu_ctx *c, size_t k) {
+  const Slot &s = c->slots[k];
+  const DoorSlot ds{s.d_arena, s.d_out, s.d_ej0, s.h_xfer_dev, s.h_xfer_dev + c->cfg.batch_records,
+                    s.h_arena_dev + door_desc_off(c), s.h_arena_dev + door_stat_off(c), door_desc_off(c),
+                    door_stat_off(c)};
+  HIPCHK(c, hipMemcpy(c->d_door_slots + k, &ds, sizeof ds, hipMemcpyHostToDevice));
+  return 0;
+}
+
+// The kernel has exited (or was never launched): no workgroup reads the
+// slot table or the SA table's cached state any more.
+bool door_exited(espgpu_ctx *c) {
+  if (c->door_live && hipEventQuery(c->ev_door) == hipSuccess) c->door_live = false;
+  return !c->door_live;
+}
+
+// Stop the persistent kernel and wait for it (published jobs it did not
+// claim stay in the ring for the next launch).
+void door_stop(espgpu_ctx *c) {
+  if (!c->door_live) return;
+  __atomic_store_n(&c->door_ctl->stop, 1u, __ATOMIC_SEQ_CST);
+  hipEventSynchronize(c->ev_door);
+  __atomic_store_n(&c->door_ctl->stop, 0u, __ATOMIC_SEQ_CST);
+  c->door_live = false;
+}
+
+int door_launch(espgpu_ctx *c) {
+  DoorArgs a{};
+  a.ctl = c->door_ctl_dev;
+  a.dev = c->d_door;
+  a.slots = c->d_door_slots;
+  a.nslots = (uint32_t)c->slots.size();
+  a.chunk = kDoorChunk;
+  a.idle_ticks = c->door_idle_us * 100u;     // s_memrealtime: 100 MHz
+  a.sas = c->d_sas;
+  a.gtab = c->d_gtab;
+  a.tpair = c->d_tpair;
+  a.nsas = c->cfg.max_sessions;              // unused entries are zero (mode 0): EINVAL
+  if (launch_gcm_door(a, c->door_wg, c->s_door)) return fail(c, ESPGPU_EIO, "door kernel launch failed");
+  HIPCHK(c, hipEventRecord(c->ev_door, c->s_door));
+  c->door_live = true;
+  return 0;
+}
+
+// Relaunch the kernel if it exited (idle timeout) while jobs are outstanding.
+int door_ensure(espgpu_ctx *c) {
+  return door_exited(c) ? door_launch(c) : 0;
+}
+
+int door_setup(espgpu_ctx *c) {
+  if (c->door_ctl) return 0;
+  if (c->slots.size() > kDoorRing) return fail(c, ESPGPU_EINVAL, "door: more staging slots than ring entries (%u)", kDoorRing);
+  HIPCHK(c, hipHostMalloc((void **)&c->door_ctl, sizeof(DoorCtl), hipHostMallocMapped | hipHostMallocCoherent));
+  memset(c->door_ctl, 0, sizeof(DoorCtl));
+  HIPCHK(c, hipHostGetDevicePointer((void **)&c->door_ctl_dev, c->door_ctl, 0));
+  HIPCHK(c, hipMalloc(&c->d_door, sizeof(DoorDev)));
+  HIPCHK(c, hipMemset(c->d_door, 0, sizeof(DoorDev)));
+  HIPCHK(c, hipMalloc(&c->d_door_slots, c->slots.size() * sizeof(DoorSlot)));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->s_door, hipStreamNonBlocking));
+  HIPCHK(c, hipEventCreateWithFlags(&c->ev_door, hipEventDisableTiming));
+  const uint32_t cap = 3 * c->cfg.batch_records;     // xin + 2 xout spans per record
+  for (size_t k = 0; k < c->slots.size(); ++k) {
+    Slot &s = c->slots[k];
+    if (s.xfer_cap < cap) {
+      hipHostFree(s.h_xfer);
+      s.h_xfer = nullptr;
+      s.xfer_cap = 0;
+      HIPCHK(c, hipHostMalloc((void **)&s.h_xfer, (size_t)cap * sizeof(XferSpan), hipHostMallocDefault));
+      HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_xfer_dev, s.h_xfer, 0));
+      s.xfer_cap = cap;
+    }
+    HIPCHK(c, hipMalloc(&s.d_ej0, (size_t)c->cfg.batch_records * sizeof(uint4)));
+    int e = door_write_slot(c, k);
+    if (e) return e;
+  }
+  c->door_next = 0;
+  return 0;
+}
+
+void door_free(espgpu_ctx *c) {
+  door_stop(c);
+  if (c->door_ctl) hipHostFree(c->door_ctl);
+  hipFree(c->d_door);
+  hipFree(c->d_door_slots);
+  if (c->ev_door) hipEventDestroy(c->ev_door);
+  if (c->s_door) hipStreamDestroy(c->s_door);
+  c->door_ctl = c->door_ctl_dev = nullptr;
+  c->d_door = nullptr;
+  c->d_door_slots = nullptr;
+  c->ev_door = nullptr;
+  c->s_door = nullptr;
+}
+
+bool door_done(const espgpu_ctx *c, int64_t job) {
+  const uint32_t j = (uint32_t)job;
+  return __atomic_load_n(&c->door_ctl->done[j % kDoorRing], __ATOMIC_ACQUIRE) == j + 1;
+}
+
+// A slot's span list of at least `need` entries (the door's fixed layout
+// keeps 3 x batch_records; a larger list moves the pinned buffer, so the
+// door kernel is stopped first and the device slot table rewritten).
+int xfer_reserve(espgpu_ctx *c, Slot &s, uint32_t need) {
+  if (need <= s.xfer_cap) return 0;
+  if (c->door_ctl) door_stop(c);
+  hipHostFree(s.h_xfer);
+  s.h_xfer = nullptr;
+  s.xfer_cap = 0;
+  const uint32_t cap = std::max(need, 256u) * 2;
+  HIPCHK(c, hipHostMalloc((void **)&s.h_xfer, (size_t)cap * sizeof(XferSpan), hipHostMallocDefault));
+  HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_xfer_dev, s.h_xfer, 0));
+  s.xfer_cap = cap;
+  if (c->door_ctl) return door_write_slot(c, (size_t)(&s - c->slots.data()));
+  return 0;
 }
 
 // Launch the crypto kernels for one batch of device-resident records.
@@ -444,7 +594,12 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.ej0 = c->d_ej0;
   }
   const GcmBsLaunch bs{c->gcm_bs, c->s_aux, c->ev_fork, c->ev_join};
-  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, (int)c->cfg.grid, c->gcm_lanes, st, &bs))
+  // beside a running doorbell kernel (one workgroup per CU on door_wg CUs)
+  // the other kernels take the remaining CUs: every workgroup of theirs must
+  // run for the launch to finish
+  int grid = c->cfg.grid ? (int)c->cfg.grid : 256;
+  if (c->door_live && !door_exited(c)) grid = std::max(1, grid - c->door_wg);
+  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, grid, c->gcm_lanes, st, &bs))
     return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if ((kinds & 2) && c->n_eta > 0) {
     EtaParams q{};
@@ -467,7 +622,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
                    (c->n_wctr > 0 ? 8 : 0) | (c->n_whash > 0 ? 16 : 0);
     q.two_pass_all = c->eta_fused >= 2;
     q.interleave = c->eta_fused == 3;
-    if (launch_eta(q, encrypt, ek, (int)c->cfg.grid, c->eta_fused != 0, st))
+    if (launch_eta(q, encrypt, ek, grid, c->eta_fused != 0, st))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
@@ -561,6 +716,7 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
 
 void espgpu_fini(espgpu_ctx *c) {
   if (!c) return;
+  door_free(c);
   for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux})
     if (st) hipStreamSynchronize(st);
   for (auto &s : c->slots) free_slot(s);
@@ -744,7 +900,8 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   // Requests already staged were accepted under this key: launch them now
   // (and the overflow behind them), then wait, so neither they nor flushed
   // batches see the slot reused.
-  if (c->ovf.empty()) espgpu_flush(c);
+  // (doorbell jobs have no stream to wait on: drain them)
+  if (c->ovf.empty() && !c->door_ctl) espgpu_flush(c);
   else espgpu_drain(c);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
@@ -752,6 +909,8 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   // and the ctx's last launch on any stream: a device-resident batch on the
   // caller's stream may still be reading this slot's keys
   if (c->launched) hipEventSynchronize(c->ev_last);
+  // the doorbell kernel keeps its current session's state (H^8 table in LDS)
+  door_stop(c);
   const Session &fs = c->sessions[sid];
   if (fs.mode != ESPGPU_CSP_MODE_AEAD) {
     c->n_eta--;
@@ -954,17 +1113,59 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
   // writing the statuses through the host mapping -- one launch per burst
   // instead of copy, kernel, copy (set_tuning "stage_fused"; the small-batch
   // GCM kernel, so not with gcm_lanes 4 or gcm_split forced)
-  if (small && c->stage_fused && !s.mixed && s.kinds == 1 && c->gcm_lanes != kGcmLanesPerRec && !c->gcm_split) {
-    const uint32_t need = 3 * s.nrec;
-    if (need > s.xfer_cap) {
-      hipHostFree(s.h_xfer);
-      s.h_xfer = nullptr;
-      s.xfer_cap = 0;
-      const uint32_t cap = std::max(need, 256u) * 2;
-      HIPCHK(c, hipHostMalloc((void **)&s.h_xfer, (size_t)cap * sizeof(XferSpan), hipHostMallocDefault));
-      HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_xfer_dev, s.h_xfer, 0));
-      s.xfer_cap = cap;
+  const bool one_gcm = !s.mixed && s.kinds == 1 && c->gcm_lanes != kGcmLanesPerRec && !c->gcm_split;
+  // Doorbell path (set_tuning "door"): a single-session GCM batch of up to
+  // gcm_burst records is published to the persistent kernel -- descriptors
+  // and span lists at the slot's fixed door offsets, then one 16-byte job in
+  // the ring -- with no HIP call at all; poll() sees done[] in host memory.
+  if (c->door_wg && one_gcm && s.nrec <= c->gcm_burst) {
+    int e = door_setup(c);
+    if (e) return e;
+    s.desc_off = door_desc_off(c);
+    s.stat_off = door_stat_off(c);
+    memcpy(s.h_arena + s.desc_off, s.h_desc, s.nrec * sizeof(espgpu_desc));
+    const uint64_t ha = (uint64_t)(uintptr_t)s.h_arena_dev, da = (uint64_t)(uintptr_t)s.d_arena;
+    const uint64_t dr = (uint64_t)(uintptr_t)dres;
+    XferSpan *xin = s.h_xfer, *xout = s.h_xfer + c->cfg.batch_records;
+    for (const Pending &pd : s.reqs) {
+      xin[pd.rec] = XferSpan{pd.zc ? pd.zc : ha + pd.stage_off, da + pd.stage_off, pd.stage_len, pd.rec};
+      for (int q = 0; q < 2; ++q) {
+        XferSpan &o = xout[2 * pd.rec + q];
+        if (q < pd.nspan) {
+          const Pending::Span &sp = pd.span[q];
+          o = XferSpan{dr + pd.stage_off + sp.stage_from,
+                       pd.zc ? pd.zc + sp.stage_from : ha + pd.stage_off + sp.stage_from, sp.n, pd.rec};
+        } else {
+          o = XferSpan{0, 0, 0, pd.rec};
+        }
+      }
     }
+    const uint32_t j = c->door_next++;
+    DoorJob &jb = c->door_ctl->ring[j % kDoorRing];
+    const uint32_t so = (uint32_t)(&s - c->slots.data()) | ((uint32_t)s.op << 16);
+    jb.n = s.nrec;
+    jb.slot_op = so;
+    jb.chk = s.nrec ^ so ^ (j + 1) ^ kDoorChk;
+    __atomic_store_n(&jb.seq, j + 1, __ATOMIC_RELEASE);
+    s.door_job = j;
+    s.door_t0 = now_ns();
+    // the kernel may have reached its idle timeout since the last job
+    if (!c->door_live || s.door_t0 - c->door_last_pub > (uint64_t)c->door_idle_us * 500u) {
+      e = door_ensure(c);
+      if (e) return e;
+    }
+    c->door_last_pub = s.door_t0;
+    s.timed = false;
+    s.state = SLOT_INFLIGHT;
+    c->stats.batches++;
+    c->stats.door++;
+    c->stats.zerocopy += s.nrec - s.nstaged;
+    c->cur = (c->cur + 1) % (int)c->slots.size();
+    return 0;
+  }
+  if (small && c->stage_fused && one_gcm) {
+    int e = xfer_reserve(c, s, 3 * s.nrec);
+    if (e) return e;
     const uint64_t ha = (uint64_t)(uintptr_t)s.h_arena_dev, da = (uint64_t)(uintptr_t)s.d_arena;
     const uint64_t dr = (uint64_t)(uintptr_t)dres;
     XferSpan *xin = s.h_xfer, *xout = s.h_xfer + s.nrec;
@@ -985,9 +1186,9 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
                          reinterpret_cast<const espgpu_desc *>(s.h_arena_dev + s.desc_off)};
     s.timed = GPU_TIME_SMALL;
     if (s.timed) hipEventRecord(s.k0, s_k);
-    int e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
-                      dres + s.stat_off, s.op ? nullptr : s.d_out, (uint32_t)ESPGPU_BATCH_GROUPED, s.op, s_k,
-                      nullptr, 1u, &stg);
+    e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
+                  dres + s.stat_off, s.op ? nullptr : s.d_out, (uint32_t)ESPGPU_BATCH_GROUPED, s.op, s_k,
+                  nullptr, 1u, &stg);
     if (e) return e;
     if (s.timed) hipEventRecord(s.k1, s_k);
     HIPCHK(c, hipEventRecord(s.done, s_k));
@@ -1015,14 +1216,9 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
     nin += pieces(s.stat_off - s.desc_off);
     nout += pieces(s.nrec);
   }
-  if (nin + nout > s.xfer_cap) {
-    hipHostFree(s.h_xfer);
-    s.h_xfer = nullptr;
-    s.xfer_cap = 0;
-    const uint32_t cap = std::max(nin + nout, 256u) * 2;
-    HIPCHK(c, hipHostMalloc((void **)&s.h_xfer, (size_t)cap * sizeof(XferSpan), hipHostMallocDefault));
-    HIPCHK(c, hipHostGetDevicePointer((void **)&s.h_xfer_dev, s.h_xfer, 0));
-    s.xfer_cap = cap;
+  {
+    int e = xfer_reserve(c, s, nin + nout);
+    if (e) return e;
   }
   uint32_t k = 0;
   auto add = [&](uint64_t src, uint64_t dst, uint32_t n, uint32_t rec) {
@@ -1136,11 +1332,26 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
 int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
   if (!c) return -ESPGPU_EINVAL;
   // completions of flushed batches, oldest first
+  bool door_wait = false;
+  const uint64_t now = c->door_ctl ? now_ns() : 0;
   for (size_t k = 0; k < c->slots.size(); ++k) {
     Slot &s = c->slots[(c->cur + k) % c->slots.size()];
     if (s.state != SLOT_INFLIGHT) continue;
-    if (hipEventQuery(s.done) != hipSuccess) continue;
+    if (s.door_job >= 0) {
+      if (!door_done(c, s.door_job)) {
+        // outstanding for over 1 ms: make sure the kernel is still there
+        door_wait |= now - s.door_t0 > 1000000u;
+        continue;
+      }
+      s.door_job = -1;
+    } else if (hipEventQuery(s.done) != hipSuccess) {
+      continue;
+    }
     complete_slot(c, s);
+  }
+  if (door_wait) {
+    int e = door_ensure(c);
+    if (e) return -e;
   }
   const int avail = (int)(c->ready.size() - c->ready_head);
   const int n = std::min(max, avail);
@@ -1162,7 +1373,19 @@ int espgpu_drain(espgpu_ctx *c) {
     for (size_t k = 0; k < c->slots.size(); ++k) {
       Slot &s = c->slots[(c->cur + k) % c->slots.size()];
       if (s.state != SLOT_INFLIGHT) continue;
-      HIPCHK(c, hipEventSynchronize(s.done));
+      if (s.door_job >= 0) {
+        // the persistent kernel's job: spin on done[], relaunching the
+        // kernel if it exited; a job the GPU never finishes is an error
+        const uint64_t t0 = now_ns();
+        while (!door_done(c, s.door_job)) {
+          int e = door_ensure(c);
+          if (e) return e;
+          if (now_ns() - t0 > 10000000000ull) return fail(c, ESPGPU_EIO, "door job %lld not done after 10 s", (long long)s.door_job);
+        }
+        s.door_job = -1;
+      } else {
+        HIPCHK(c, hipEventSynchronize(s.done));
+      }
       complete_slot(c, s);
     }
   } while (!c->ovf.empty());     // the overflow goes into the slots just freed
@@ -1424,6 +1647,24 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!strcmp(key, "xfer")) {
     if (value != 0 && value != 1) return ESPGPU_EINVAL;
     c->xfer_small = value;
+    return 0;
+  }
+  if (!strcmp(key, "door")) {
+    // workgroups of the doorbell kernel (0 = off); changing it drains and
+    // stops the running kernel (the next batch relaunches it)
+    if (value < 0 || value > 256) return ESPGPU_EINVAL;
+    if (value != c->door_wg && c->door_ctl) {
+      int e = espgpu_drain(c);
+      if (e) return e;
+      door_stop(c);
+    }
+    c->door_wg = value;
+    return value ? door_setup(c) : 0;
+  }
+  if (!strcmp(key, "door_idle_us")) {
+    if (value < 100 || value > 10000000) return ESPGPU_EINVAL;
+    door_stop(c);
+    c->door_idle_us = (uint32_t)value;
     return 0;
   }
   if (!strcmp(key, "gcm_opts")) return set_gcm_opts((uint32_t)value) ? ESPGPU_ENOTSUP : 0;

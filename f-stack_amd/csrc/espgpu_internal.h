@@ -154,7 +154,62 @@ struct XferSpan {
 };
 constexpr uint32_t kXferPiece = 4096;
 
+// ---- doorbell burst path (set_tuning "door", esp_gcm.hip gcm_door_kernel) ----
+// A persistent kernel of `door` workgroups (one per CU) serves the process
+// path's single-session GCM bursts without a launch per burst: flush writes a
+// 16-byte job into a ring in pinned host memory, the workgroups poll it over
+// the mapping, claim the job's chunks from a device counter, stage the
+// records in and the results out as the burst kernel does, and the workgroup
+// finishing a job's last chunk writes its number into done[] (host memory),
+// which poll() reads.  The kernel exits when the host sets stop or after
+// idle_ticks of s_memrealtime (100 MHz) without a job; poll() relaunches it
+// when a job is outstanding and it has exited.
+constexpr uint32_t kDoorRing = 64;              // job ring entries (>= staging slots)
+struct DoorJob {                                 // host-written; seq last (= job number + 1)
+  uint32_t n;                                    // records
+  uint32_t slot_op;                              // staging slot | op << 16 (0 decrypt, 1 encrypt)
+  uint32_t chk;                                  // n ^ slot_op ^ seq ^ kDoorChk: a torn read never matches
+  uint32_t seq;
+};
+constexpr uint32_t kDoorChk = 0x5eed1e55u;
+struct DoorCtl {                                 // pinned host memory, device-mapped
+  DoorJob ring[kDoorRing];
+  uint32_t stop;
+  uint32_t pad_[31];
+  uint32_t done[kDoorRing];                      // job number + 1 once the job completed
+};
+struct DoorDev {                                 // device memory, zeroed once
+  // per ring entry: (job + 1) << 32 | chunks claimed.  A workgroup installs
+  // job j's generation (CAS from an older one) only after it has seen job j
+  // published, then claims with an atomic add; an add that lands on a later
+  // job's generation holds that job's chunk (it is published), so no claim
+  // is ever lost and none waits on an unpublished job.
+  unsigned long long tick[kDoorRing];
+  uint32_t fin[kDoorRing];                       // chunks finished, per ring entry
+  uint32_t next;                                 // lowest job not known to be fully claimed (a hint)
+};
+struct DoorSlot {                                // per staging slot (device table)
+  uint8_t *arena, *out;                          // out: decrypt results (encrypt: in place)
+  uint4 *ej0;
+  const struct XferSpan *xin, *xout;             // xin[i]; xout[2i], xout[2i+1]
+  uint8_t *hdesc, *hstat;                        // host descriptors / statuses (mapped)
+  uint32_t desc_off, stat_off;                   // device descriptors and statuses in arena / out
+};
+struct DoorArgs {
+  DoorCtl *ctl;                                  // device-mapped address
+  DoorDev *dev;
+  const DoorSlot *slots;
+  uint32_t nslots;
+  uint32_t chunk;                                // records per chunk
+  uint32_t idle_ticks;
+  const DevSA *sas;
+  const uint8_t *gtab;
+  const uint2 *tpair;
+  uint32_t nsas;
+};
+
 // Launchers (defined in the .hip files, called by espgpu.cpp).
+int launch_gcm_door(const DoorArgs &a, int grid, void *stream);
 // lanes: 0 = by batch size (kGcmLanesSmall below kGcmSmallBatch records,
 // else kGcmLanesPerRec), or force 4 / 8 (set_tuning "gcm_lanes", tests)
 // The bitsliced ctr pass for large batches (set_tuning "gcm_bs"): mode 0 off,

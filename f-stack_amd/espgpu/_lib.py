@@ -92,7 +92,8 @@ class Config(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("bytes", C.c_uint64), ("auth_fail", C.c_uint64),
                 ("einval", C.c_uint64), ("batches", C.c_uint64), ("kernel_ns", C.c_uint64),
-                ("erestart", C.c_uint64), ("overflow", C.c_uint64), ("zerocopy", C.c_uint64)]
+                ("erestart", C.c_uint64), ("overflow", C.c_uint64), ("zerocopy", C.c_uint64),
+                ("door", C.c_uint64)]
 
 
 _lib = None

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define ESPGPU_ABI_VERSION 2
+#define ESPGPU_ABI_VERSION 3
 
 /* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
 #define ESPGPU_CSP_MODE_CIPHER      2        /* cryptodev.h:362: ESP without auth */
@@ -160,6 +160,7 @@ struct espgpu_stats {
 	uint64_t erestart;
 	uint64_t overflow;             /* requests staged through the host overflow      */
 	uint64_t zerocopy;             /* records moved from / to registered memory      */
+	uint64_t door;                 /* batches served by the doorbell kernel (ABI 3)  */
 };
 
 typedef struct espgpu_ctx espgpu_ctx;
@@ -367,6 +368,17 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *               run the small-batch design, out of place or encrypt, use the
  *               burst kernel (a 32-lane CTR pass and an 8-lane GHASH in one
  *               launch, for latency); 0 = the fused small-batch kernel;
+ *   "door"      doorbell path (0, the default: off): N > 0 keeps a
+ *               persistent kernel of N workgroups (one per CU) resident that
+ *               serves the process path's single-session GCM batches of up
+ *               to gcm_burst records -- flush() publishes a 16-byte job in
+ *               pinned host memory instead of launching, the kernel stages
+ *               the records in and the results out through the mapping, and
+ *               poll() reads its done word -- so a burst pays no launch or
+ *               completion signal; other kernels of the ctx then use the
+ *               remaining CUs; 1..256, others EINVAL; changing it drains;
+ *   "door_idle_us" the doorbell kernel exits after this long without a
+ *               job (default 20000; 100..10^7): flush / poll relaunch it;
  *   "stage_fused" a process-path burst of one GCM session stages its own
  *               records inside the crypto kernel (1, default: one launch per
  *               burst) instead of xfer kernels around it (0);

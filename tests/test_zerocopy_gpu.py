@@ -390,3 +390,176 @@ def test_single_session_gcm_burst_self_staging(fused, burst, esn):
         fw.crypto_freesession(cs)
     finally:
         drv.close()
+
+
+def _gcm_burst_round(fw, cs, sa_obj, rng, n, reg, sizes=(4, 12, 100, 1448), esn_hi=True):
+    """One encrypt + tampered-decrypt round of n single-session GCM records
+    through the driver path, records in `reg` (registered) or their own
+    buffers, checked against the oracle."""
+    sas = [sa_obj]
+    idx = np.zeros(n, dtype=np.int64)
+    eh = rng.integers(0, 2**32, n, dtype=np.uint32) if esn_hi else None
+    plain, ct, descs, eh = build_records(rng, sas, idx, rng.choice(sizes, n), esn_hi=eh)
+    lay = _Layout(rng, descs, n, reg, frac_reg=0.6)
+    sa = sa_obj.esp_sa()
+    for i in range(n):
+        lay.put(i, plain)
+    crps = [esp_output(fw, cs, sa, lay.pkt(i), lay.skip, int(eh[i])) for i in range(n)]
+    _run(fw, crps)
+    for i in range(n):
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        assert crps[i].crp_etype == 0 and lay.get(i) == bytes(ct[o:o + L]), (n, i)
+    bad = set(int(i) for i in rng.choice(n, max(1, n // 8), replace=False))
+    before = {}
+    for i in range(n):
+        lay.put(i, ct)
+        if i in bad:
+            lay.pkt(i)[lay.skip + int(descs["len"][i]) - 2] ^= 0x01
+            before[i] = lay.get(i)
+    crps = [esp_input(fw, cs, sa, lay.pkt(i), lay.skip, int(eh[i])) for i in range(n)]
+    _run(fw, crps)
+    for i in range(n):
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        if i in bad:
+            assert crps[i].crp_etype == O.EBADMSG and lay.get(i) == before[i], (n, i)
+        else:
+            assert crps[i].crp_etype == 0, (n, i)
+            assert lay.get(i)[16:L - sa.mlen] == bytes(plain[o + 16:o + L - sa.mlen]), (n, i)
+
+
+def esp_output(fw, cs, sa, pkt, skip, eh):
+    from espgpu.esp import esp_output_crp
+    return esp_output_crp(fw, cs, sa, pkt, skip, esn_hi=eh)
+
+
+def esp_input(fw, cs, sa, pkt, skip, eh):
+    from espgpu.esp import esp_input_crp
+    return esp_input_crp(fw, cs, sa, pkt, skip, esn_hi=eh)
+
+
+@pytest.mark.parametrize("wg", [8, 64])
+@pytest.mark.parametrize("esn", [False, True])
+def test_door_burst_vs_oracle(wg, esn):
+    """The doorbell path (set_tuning "door"): single-session GCM batches are
+    published to the persistent kernel (a 16-byte job in pinned host memory,
+    no launch) which stages the records in from registered memory or the
+    pinned staging buffer, runs the burst design per claimed 4-record chunk
+    and writes results, statuses and the job's done word back.  Encrypt and
+    tampered decrypt vs the oracle at 1 .. 600 records per batch (1 .. 150
+    chunks over `wg` workgroups); every batch went through the door."""
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=4)
+    try:
+        assert drv.set_tuning("door", wg) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2600 + wg + esn)
+        sa = GcmSA(rng, 16 if not esn else 32, esn=esn, mlen=16 if not esn else 12)
+        err, cs = fw.crypto_newsession(sa.esp_sa().csp())
+        assert err == 0
+        reg = np.zeros(1 << 21, dtype=np.uint8)
+        drv.register_host(reg)
+        d0, b0 = drv.stats()["door"], drv.stats()["batches"]
+        for n in (1, 32, 77, 600):
+            _gcm_burst_round(fw, cs, sa, rng, n, reg)
+        s = drv.stats()
+        assert s["door"] - d0 == s["batches"] - b0 > 0
+        drv.unregister_host(reg)
+        fw.crypto_freesession(cs)
+    finally:
+        drv.close()
+
+
+def test_door_relaunch_and_mixed_batches():
+    """The doorbell kernel exits after door_idle_us without a job and the next
+    flush relaunches it; a batch the door does not serve (several sessions,
+    ETA) runs as launched kernels beside it on the remaining CUs; freeing a
+    session stops the kernel (its LDS holds the session's GHASH table) and the
+    next burst relaunches it.  Every round vs the oracle."""
+    import time
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=16)
+    try:
+        assert drv.set_tuning("door", 32) == 0
+        assert drv.set_tuning("door_idle_us", 300) == 0
+        assert drv.set_tuning("door_idle_us", 50) == 22
+        assert drv.set_tuning("door", 257) == 22
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2700)
+        sa = GcmSA(rng, 16)
+        err, cs = fw.crypto_newsession(sa.esp_sa().csp())
+        assert err == 0
+        reg = np.zeros(1 << 21, dtype=np.uint8)
+        drv.register_host(reg)
+        d0 = drv.stats()["door"]
+        _gcm_burst_round(fw, cs, sa, rng, 32, reg)
+        time.sleep(0.02)                                  # > door_idle_us: the kernel has exited
+        _gcm_burst_round(fw, cs, sa, rng, 40, reg)
+        # mixed sessions: launched kernels (grid reduced beside the door kernel)
+        sas = _sas(rng)
+        ses = [fw.crypto_newsession(s.esp_sa().csp())[1] for s in sas]
+        n = 60
+        idx = rng.integers(0, len(sas), n)
+        plain, ct, descs, eh = build_records(rng, sas, idx, _cts(rng, sas, idx))
+        pkts = []
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            pkts.append(bytearray(bytes(ct[o:o + L])))
+        crps = [esp_input(fw, ses[idx[i]], sas[idx[i]].esp_sa(), pkts[i], 0, 0) for i in range(n)]
+        _run(fw, crps)
+        for i in range(n):
+            s_ = sas[idx[i]]
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert crps[i].crp_etype == 0, i
+            assert bytes(pkts[i][s_.hlen:L - s_.mlen]) == bytes(plain[o + s_.hlen:o + L - s_.mlen]), i
+        _gcm_burst_round(fw, cs, sa, rng, 32, reg)
+        for s_ in ses:
+            fw.crypto_freesession(s_)                     # stops the door kernel
+        _gcm_burst_round(fw, cs, sa, rng, 32, reg)
+        assert drv.stats()["door"] - d0 == 8
+        drv.unregister_host(reg)
+        fw.crypto_freesession(cs)
+    finally:
+        drv.close()
+
+
+def test_door_fstack_loop_with_overflow():
+    """F-Stack's main_loop shape on the doorbell path: 4-record slots, two of
+    them, a 1-MiB overflow; 400 requests arrive 8 per iteration, each
+    iteration flushes and polls once and never waits.  Several jobs are in
+    flight at once; completions come back in arrival order, bit-exact."""
+    from espgpu.opencrypto import CryptoFramework
+    drv = _driver(max_sessions=4, batch_records=4, nbatches=2)
+    try:
+        assert drv.set_tuning("overflow_mb", 1) == 0
+        assert drv.set_tuning("door", 16) == 0
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2800)
+        n = 400
+        sas = [GcmSA(rng, 16)]
+        idx = np.zeros(n, dtype=np.int64)
+        plain, ct, descs, eh = build_records(rng, sas, idx, rng.choice([100, 1448], n))
+        cs = fw.crypto_newsession(sas[0].esp_sa().csp())[1]
+        pkts = []
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            pkts.append(bytearray(bytes(ct[o:o + L])))
+        crps = [esp_input(fw, cs, sas[0].esp_sa(), pkts[i], 0, 0) for i in range(n)]
+        order, spins, d0 = [], 0, drv.stats()["door"]
+        for i in range(0, n, 8):
+            for c in crps[i:i + 8]:
+                assert drv.process(c) == 0
+            drv.flush()
+            order += [id(c) for c in drv.poll()]
+        while len(order) < n:
+            drv.flush()
+            order += [id(c) for c in drv.poll()]
+            spins += 1
+            assert spins < 10**7
+        assert order == [id(c) for c in crps]
+        assert drv.stats()["door"] - d0 >= n // 4
+        for i in range(n):
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert crps[i].crp_etype == 0
+            assert bytes(pkts[i][16:L - 16]) == bytes(plain[o + 16:o + L - 16])
+    finally:
+        drv.close()

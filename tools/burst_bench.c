@@ -277,13 +277,13 @@ int main(int argc, char **argv)
 				const double df = pipelined(B, iters, 1, &bad, &wf);
 				CK(espgpu_set_tuning(ctx, "overflow_mb", 0));
 				CK(espgpu_get_stats(ctx, &s1));
-				printf("{\"burst\": %d, \"mode\": \"%s\", \"xfer\": %d, \"record_bytes\": %d, "
+				printf("{\"burst\": %d, \"tuning\": \"%s\", \"mode\": \"%s\", \"xfer\": %d, \"record_bytes\": %d, "
 				       "\"latency_us_median\": %.1f, \"latency_us_p99\": %.1f, \"latency_records_per_s\": %.0f, "
 				       "\"pipelined_records_per_s\": %.0f, \"pipelined_GBps\": %.3f, "
 				       "\"fstack_records_per_s\": %.0f, \"fstack_GBps\": %.3f, \"fstack_max_process_us\": %.1f, "
 				       "\"batches\": %llu, \"overflow\": %llu, \"zerocopy\": %llu, "
 				       "\"iters\": %d, \"auth_fail\": [%d, %d]}\n",
-				       B, mode ? "registered" : "gather", xfer, REC, med, p99, B / med * 1e6,
+				       B, tun ? tun : "", mode ? "registered" : "gather", xfer, REC, med, p99, B / med * 1e6,
 				       iters * (double)B / dt * 1e6, iters * (double)B * REC / dt / 1e3,
 				       iters * (double)B / df * 1e6, iters * (double)B * REC / df / 1e3, wf,
 				       (unsigned long long)(s1.batches - s0.batches),
