@@ -78,6 +78,11 @@
 #ifndef GCM_OUTALIGN
 #define GCM_OUTALIGN 0
 #endif
+// Output ring (MODE 0, S = 4, 1024-thread workgroups): plaintext goes through
+// a 128-byte LDS line buffer per record and leaves as whole 128-byte lines
+#ifndef GCM_RING
+#define GCM_RING 0
+#endif
 
 namespace espgpu {
 
@@ -88,6 +93,10 @@ namespace {
 constexpr uint32_t LDS_GT = 0;          // H^S, 256 values x 16 positions x 16 B
 constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
 constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
+// The output ring after them (gcm_kernel with RING): 128 bytes per record in
+// flight, 256 records per workgroup = the 32 KiB the tables leave of 160 KiB.
+constexpr uint32_t LDS_RING = LDS_BYTES;
+constexpr uint32_t kRingBytes = 128 * 256;
 
 // Round keys are read through the constant address space: uniform loads from
 // it become s_load (SGPRs, scalar cache) instead of vector loads or LDS reads.
@@ -122,6 +131,28 @@ __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
 __device__ __forceinline__ void st8(uint8_t *p, uint32_t a, uint32_t b) {
   V2a u = {a, b};
   *reinterpret_cast<V2a *>(p) = u;
+}
+
+// LDS writes at an explicit LDS byte address; ds_w128 at 4-byte alignment
+// relies on the unaligned LDS mode (tools/ldsalign.hip checks it on the
+// device), which the compiler does not assume: it would split the access.
+__device__ __forceinline__ void ds_w128(uint32_t addr, uint4 v) {
+  typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+  const V4 u = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(u) : "memory");
+}
+__device__ __forceinline__ void ds_w32(uint32_t addr, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+// the ring's block writes: one ds_write_b128 (GCM_RING 1) or four dword
+// writes (GCM_RING 2)
+__device__ __forceinline__ void ring_w16(uint32_t addr, uint4 v) {
+#if GCM_RING == 2
+  asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %0, %2 offset:4\n\tds_write_b32 %0, %3 offset:8\n\tds_write_b32 %0, %4 offset:12"
+               ::"v"(addr), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w) : "memory");
+#else
+  ds_w128(addr, v);
+#endif
 }
 
 // Keep the first `rem` bytes of a 16-byte block, zero the rest.  Valid ESP
@@ -541,7 +572,7 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
 // Steps m, m+1 of a lane run together: 2 independent AES blocks, then
 // GHASH as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with the 8-bit table.
-template <int MODE, int S>
+template <int MODE, int S, bool RING = false>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
                                          uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk) {
   const int lane = threadIdx.x & 63;
@@ -611,6 +642,95 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       trl = esp_trailer_word(rem >= 16 ? pt.w : (rem > 8 ? pt.z : (rem > 4 ? pt.y : pt.x)),
                              (uint32_t)ct_len);
   };
+
+  // Output ring (RING, aligned schedule): the plaintext leaves as whole
+  // 128-byte lines.  AES pair step a (a even) produces the record's window
+  // [64a, 64a + 128) of plaintext, lane l blocks 4a + l and 4a + 4 + l (window
+  // offsets 16l and 64 + 16l).  The record's 128-byte LDS buffer holds the
+  // line at P + 64a (P = plaintext start) by address mod 128: write phase 1
+  // puts the window's bytes of that line (positions [r, 128), r = P mod 128)
+  // beside the r bytes the previous step left at [0, r); the four lanes read
+  // the whole line back (two aligned ds_read_b128 each) and store it with
+  // aligned 16-byte stores, only the plaintext bytes of the record's first and
+  // last lines dword by dword; write phase 2 then puts the window's bytes of
+  // the next line at [0, r).  Bytes past the plaintext (the J0 slot, a partial
+  // last block, idle lanes) land only on positions that are never stored.
+  // Writes are ds_write_b128 at 4-byte alignment (the unaligned LDS mode of
+  // gfx950, tools/ldsalign.hip); the one block per record that crosses the
+  // line boundary goes dword by dword.  Record i of the wave reads its line's
+  // halves in swapped order when bit 1 of i is set, so every ds_read_b128 of
+  // the line is conflict-free (16-lane groups see 16 distinct bank quads).
+  // P, r and the buffer offset are recomputed where they are used, from
+  // registers the loop keeps anyway (rec, di, the lane id): held across the
+  // loop they would be spilled (the kernel is at its 128-VGPR cap)
+  auto ring_P = [&]() -> uint8_t * {
+    uintptr_t rv = (uintptr_t)rec;
+    uint32_t dv = di;
+    asm volatile("" : "+v"(rv), "+v"(dv));
+    return p.out_stride ? p.out + (size_t)dv * p.out_stride : (uint8_t *)rv + (p.out - p.arena) + 16;
+  };
+  auto ring_off = [&]() -> uint32_t {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return LDS_RING + (t >> 2) * 128u;   // S == 4
+  };
+  // the line at P + 64a: its two 16-byte chunks of this lane from the ring
+  // (ring_read), then to memory (ring_store), plaintext bytes only
+  auto ring_read = [&](uint4 &v0, uint4 &v1) {
+    const uint32_t ro = ring_off();
+    const uint32_t c0 = (16u * (uint32_t)l + (((uint32_t)lane >> 3) & 1u) * 64u) & 127u;
+    v0 = *reinterpret_cast<const uint4 *>(lds + ro + c0);
+    v1 = *reinterpret_cast<const uint4 *>(lds + ro + (c0 ^ 64u));
+  };
+  auto ring_store = [&](int a, uint4 v0, uint4 v1) {
+    if (!valid) return;
+    const uint32_t c0 = (16u * (uint32_t)l + (((uint32_t)lane >> 3) & 1u) * 64u) & 127u;
+    uint8_t *const P = ring_P();
+    uint8_t *const Lc = (uint8_t *)(((uintptr_t)P + 64u * (uint32_t)a) & ~(uintptr_t)127);
+    const int rel0 = (int)(Lc - P);                          // line start relative to P
+    auto put = [&](uint32_t c, uint4 v) {
+      const int lo = rel0 + (int)c;
+      if (lo >= 0 && lo + 16 <= ct_len) {
+        *reinterpret_cast<uint4 *>(Lc + c) = v;
+      } else if (lo + 16 > 0 && lo < ct_len) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (lo + 4 * k >= 0 && lo + 4 * k < ct_len) reinterpret_cast<uint32_t *>(Lc + c)[k] = w[k];
+      }
+    };
+    put(c0, v0);
+    put(c0 ^ 64u, v1);
+  };
+  auto ring_step = [&](int a, uint4 Oa, uint4 Ob) {
+    const uint32_t rb = (uint32_t)(uintptr_t)(lds + ring_off());   // LDS address of the buffer
+    const uint32_t sa_ = ((uint32_t)(uintptr_t)ring_P() & 127u) + 16u * (uint32_t)l, sb_ = sa_ + 64u;
+    const bool sta = sa_ < 128u && sa_ + 16u > 128u, stb = sb_ < 128u && sb_ + 16u > 128u;
+    const bool st = sta || stb;
+    const uint4 X = sta ? Oa : Ob;
+    const uint32_t sx = sta ? sa_ : sb_;
+    // phase 1: the bytes of the current line
+    if (sa_ + 16u <= 128u) ring_w16(rb + sa_, Oa);
+    if (sb_ + 16u <= 128u) ring_w16(rb + sb_, Ob);
+    if (st) ds_w32(rb + sx, X.x);
+    if (st && sx <= 120u) ds_w32(rb + sx + 4u, X.y);
+    if (st && sx == 116u) ds_w32(rb + sx + 8u, X.z);
+    uint4 v0, v1;
+    ring_read(v0, v1);
+    // phase 2: the bytes of the next line (the reads above are served first:
+    // a wave's LDS instructions execute in order)
+    if (sa_ >= 128u) ring_w16(rb + sa_ - 128u, Oa);
+    if (sb_ >= 128u) ring_w16(rb + sb_ - 128u, Ob);
+    if (st) ds_w32(rb + sx + 12u - 128u, X.w);
+    if (st && sx >= 120u) ds_w32(rb + sx + 8u - 128u, X.z);
+    if (st && sx == 124u) ds_w32(rb + sx + 4u - 128u, X.y);
+    ring_store(a, v0, v1);
+  };
+  auto ring_line = [&](int a) {
+    uint4 v0, v1;
+    ring_read(v0, v1);
+    ring_store(a, v0, v1);
+  };
   // GHASH input block of GHASH index i (>= 1) given its ciphertext C and
   // keystream ks; stores the output block (MODE 0: plaintext, MODE 1: CT).
   auto block_in = [&](int i, bool has_ct, uint4 C, uint4 ks) -> uint4 {
@@ -670,7 +790,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       }
       const int rem = ct_len - 16 * j;
       const uint4 o = xor4(C, ks);
-      if (!(gopts() & 9)) st_partial(orec + 16 + 16 * j, o, rem);
+      if (!RING && !(gopts() & 9)) st_partial(orec + 16 + 16 * j, o, rem);
       if (MODE == 0) note_trailer(j + 1, o, rem);
       return mask_block(MODE == 1 ? o : C, rem);
     };
@@ -692,7 +812,9 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
           uint4 ka, kb;
           aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
           const uint4 Oa = xor4(Ca, ka), Ob = xor4(Cb, kb);
-          if (valid && !(gopts() & 9)) {
+          if (RING) {
+            ring_step(a, Oa, Ob);
+          } else if (valid && !(gopts() & 9)) {
             st16(orec + 16 + 16 * ja, Oa);
             st16(orec + 16 + 16 * jb, Ob);
           }
@@ -712,13 +834,15 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       // (the edge steps of a record: one block at a time, so the general path
       // holds one keystream block and inlines no second pair round)
       if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
-      const uint4 Ba = a < Ma ? slot_out(ja, Ca, aes_ctr(cc, ca, rk3, nr, rk, lds, slot)) : make_uint4(0, 0, 0, 0);
-      uint4 Bb = make_uint4(0, 0, 0, 0);
+      const uint4 ka = aes_ctr(cc, ca, rk3, nr, rk, lds, slot);
+      const uint4 Ba = a < Ma ? slot_out(ja, Ca, ka) : make_uint4(0, 0, 0, 0);
+      uint4 Bb = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
       if (two) {
         if ((int)(cb >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(cb >> 8), rk, lds, slot);
-        const uint4 kb = aes_ctr(cc, cb, rk3, nr, rk, lds, slot);
+        kb = aes_ctr(cc, cb, rk3, nr, rk, lds, slot);
         if (a + 1 < Ma) Bb = slot_out(jb, Cb, kb);
       }
+      if (RING) ring_step(a, xor4(Ca, ka), xor4(Cb, kb));
       // GHASH steps a (block prev) and a + 1 (block Ba), each only if <= Ma
       const uint4 Ym = a == 0 ? prev : xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), prev);
       if (valid && a <= Ma) Y = Ym;
@@ -731,6 +855,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       const uint4 Yn = xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), prev);
       if (valid && Ma == Maw) Y = Yn;
     }
+    // the line the last window ended in
+    if (RING) ring_line((Maw + 1) & ~1);
   }
   while (m < Mw) {
     const int i = S * m + l - pad;
@@ -1321,7 +1447,9 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   static_assert(S == kGcmLanesPerRec || S == kGcmLanesSmall, "GHASH tables exist for these strides");
   constexpr int RPW = 64 / S;             // records per wave
   constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  // the output ring (do_group): the headline decrypt's shape only
+  constexpr bool RING = GCM_RING && MODE == 0 && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0)];
   const int tid = threadIdx.x;
   GCM_PHASE(0, true);
 
@@ -1343,12 +1471,17 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // balances the chip where a static split would leave most CUs idle.
   // s_ticket is double-buffered by iteration parity: slot it&1 is rewritten
   // only at it+2, after every thread passed iteration it+1's barrier.
-  __shared__ uint32_t s_ticket[2];
+  // With the ring no LDS byte is left for it: the ticket goes through the
+  // first ring line (tid 0's own record, idle between groups) and a second
+  // barrier keeps it until every wave has read it.
+  __shared__ uint32_t s_ticket[RING ? 1 : 2];
   __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
   for (uint32_t it = 0;; ++it) {
-    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
+    uint32_t *tk = RING ? reinterpret_cast<uint32_t *>(lds + LDS_RING) : s_ticket + (it & 1);
+    if (tid == 0) *tk = atomicAdd(&p.queue[0], 1u);
     __syncthreads();
-    const uint32_t c = s_ticket[it & 1];
+    const uint32_t c = *tk;
+    if (RING) __syncthreads();
     GCM_PHASE(2, it == 0);
     if (c >= nch) break;
     uint32_t sa, start, count;
@@ -1408,7 +1541,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         continue;
       }
-      do_group<MODE, S>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
+      do_group<MODE, S, RING>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
     }
     GCM_PHASE(5, it == 0);
     if (STAGE) {
