@@ -1003,8 +1003,14 @@ __device__ __forceinline__ bool eta_interleaved(const EtaParams &p, const uint8_
 // CKS: MODE 0 is built once per cipher (CK_CBC / CK_CTR) and each launch
 // serves only its cipher's sessions -- both fused paths inlined in one kernel
 // made the register allocator spill; -1 = every ETA session.
+#ifndef ETA_C8_WG
+#define ETA_C8_WG 512
+#endif
+#ifndef ETA_C6_VGPR
+#define ETA_C6_VGPR 512
+#endif
 template <int MODE, int WG, int CKS>
-__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
+__device__ __forceinline__ void eta_body(const EtaParams &p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
@@ -1071,7 +1077,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         have = false;                                       // the other cipher's pass / no cipher
       } else if (MODE == 3 && !two_pass_only(s->calg, s->aalg) && !p.two_pass_all) {
         have = false;                                       // the fused launches' session
-      } else if ((MODE == 5 || MODE == 6) && two_pass_only(s->calg, s->aalg)) {
+      } else if ((MODE == 5 || MODE == 6 || MODE == 8) && two_pass_only(s->calg, s->aalg)) {
         have = false;                                       // MODE 3's session
       } else if ((MODE == 2 || MODE == 3 || MODE == 7) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
                                               (CKS == CK_WIDEH && !wide_hash(s->aalg)))) {
@@ -1087,7 +1093,8 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         valid = pl > 0 && (ctr || null || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
         if (valid && MODE == 5) ok = p.status[di] == ESPGPU_OK;   // verified by the MODE 6 pass
-        if (valid && (MODE == 2 || MODE == 3 || MODE == 7) && s->aalg == 0) {
+        if (valid && MODE == 8) ok = true;          // decrypt every valid record (MODE 6 verifies beside it)
+        if (valid && (MODE == 2 || MODE == 3 || MODE == 6 || MODE == 7) && s->aalg == 0) {
           ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
         } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
@@ -1238,7 +1245,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
       continue;
     }
-    if (have && MODE != 5) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+    if (have && MODE != 5 && MODE != 8) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
     // trailer word: 0 now for records that will not be decrypted; the lane
     // decrypting a record's last block writes the others'
     if (have && p.trailer && !(valid && ok)) p.trailer[di] = 0;
@@ -1351,6 +1358,17 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   }
 }
 
+template <int MODE, int WG, int CKS>
+__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
+  eta_body<MODE, WG, CKS>(p);
+}
+// the concurrent design's verify pass, with a register cap so that it fits
+// beside the decrypt waves (eta_fused 4)
+template <int WG>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_num_vgpr(ETA_C6_VGPR))) void eta_verify_kernel(EtaParams p) {
+  eta_body<6, WG, -1>(p);
+}
+
 }  // namespace
 
 int set_eta_opts(uint32_t opts) {
@@ -1363,7 +1381,14 @@ int set_eta_opts(uint32_t opts) {
 
 // 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
 // schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
-int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream) {
+// The concurrent design's trailer merge: MODE 8 wrote a trailer word for
+// every valid record, MODE 6 the statuses; a record that failed keeps 0.
+__global__ __launch_bounds__(256) void eta_trailer_merge(const uint8_t *status, uint32_t *trailer, uint32_t n) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    if (status[i] != ESPGPU_OK) trailer[i] = 0;
+}
+
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream, const EtaAux *aux) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   // implicit units (64 records, one wave each): no more workgroups than units
@@ -1388,6 +1413,26 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     if (in_place) {
       hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    } else if (fused == 4 && aux) {
+      // concurrent (eta_fused 4, out of place): the verify pass (MODE 6, lane
+      // = record SHA-1 / SHA2-256 on the VALU, no LDS) on the aux stream beside
+      // the decrypt of every valid record (MODE 8, block-parallel AES on the
+      // LDS tables), sized to share each CU (2 decrypt waves + 1 verify wave
+      // per SIMD); SHA2-384/512 sessions after them (MODE 3)
+      hipStream_t sa = reinterpret_cast<hipStream_t>(aux->aux);
+      hipEvent_t ef = reinterpret_cast<hipEvent_t>(aux->ev_fork), ej = reinterpret_cast<hipEvent_t>(aux->ev_join);
+      EtaParams pv = p;
+      pv.queue = aux->queue;
+      if (hipEventRecord(ef, st) != hipSuccess || hipStreamWaitEvent(sa, ef, 0) != hipSuccess) return -1;
+      if (kinds & 3) {
+        hipLaunchKernelGGL((eta_kernel<8, ETA_C8_WG, -1>), dim3(clamp(grid, ETA_C8_WG)), dim3(ETA_C8_WG), 0, st, p);
+        hipLaunchKernelGGL((eta_verify_kernel<256>), dim3(clamp(grid, 256)), dim3(256), 0, sa, pv);
+      }
+      if (hipEventRecord(ej, sa) != hipSuccess || hipStreamWaitEvent(st, ej, 0) != hipSuccess) return -1;
+      if ((kinds & 3) && p.trailer)
+        hipLaunchKernelGGL(eta_trailer_merge, dim3(std::min(1024u, (p.n + 255) / 256)), dim3(256), 0, st, p.status,
+                           p.trailer, p.n);
+      if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
     } else if (p.two_pass_all && !p.interleave) {
       hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);

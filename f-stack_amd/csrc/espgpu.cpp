@@ -620,9 +620,10 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.nsas = nsas;
     const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wcbc > 0 ? 4 : 0) |
                    (c->n_wctr > 0 ? 8 : 0) | (c->n_whash > 0 ? 16 : 0);
-    q.two_pass_all = c->eta_fused >= 2;
+    q.two_pass_all = c->eta_fused == 2 || c->eta_fused == 3;
     q.interleave = c->eta_fused == 3;
-    if (launch_eta(q, encrypt, ek, grid, c->eta_fused != 0, st))
+    const EtaAux eaux{c->s_aux, c->ev_fork, c->ev_join, c->d_queue + 4};
+    if (launch_eta(q, encrypt, ek, grid, c->eta_fused, st, &eaux))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
@@ -1600,7 +1601,7 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   // library (make -C f-stack_amd variants): ENOTSUP here for anything but
   // the default
   if (!strcmp(key, "eta_fused")) {
-    if (value < 0 || value > 3) return ESPGPU_EINVAL;
+    if (value < 0 || value > 4) return ESPGPU_EINVAL;
     if (!kVariants && value != 2) return ESPGPU_ENOTSUP;
     c->eta_fused = value;
     return 0;

@@ -226,7 +226,14 @@ int set_eta_opts(uint32_t opts);
 // kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones
 // fused: 1 = the one-pass out-of-place decrypt (MODE 0) / verify-first
 // in-place kernel (MODE 2); 0 = verify pass + block-parallel decrypt pass
-int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream);
+// the concurrent ETA design's second stream (eta_fused 4): its own work
+// queue words, fork / join events
+struct EtaAux {
+  void *aux, *ev_fork, *ev_join;
+  uint32_t *queue;
+};
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream,
+               const EtaAux *aux = nullptr);
 int launch_replay_check(const uint8_t *arena, espgpu_desc *desc, uint32_t n, const espgpu_replay *rp,
                         uint32_t nrp, const uint32_t *bitmap, uint8_t *rstatus, void *stream);
 int launch_xfer(const XferSpan *spans, uint32_t nspans, const uint8_t *status, void *stream);

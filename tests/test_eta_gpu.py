@@ -225,7 +225,7 @@ def _mask_var(descs, size, hl, ml):
 
 
 @pytest.mark.parametrize("fused", [2, pytest.param(3, marks=variants_only), pytest.param(1, marks=variants_only),
-                                   pytest.param(0, marks=variants_only)])
+                                   pytest.param(0, marks=variants_only), pytest.param(4, marks=variants_only)])
 @pytest.mark.parametrize("esn", [False, True])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
@@ -235,7 +235,8 @@ def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
     untouched in place.  fused (set_tuning eta_fused): 2 = the default
     two-pass MODE 3 kernel out of place, 3 = verify and decrypt interleaved
     (MODE 7), 1 = the one-pass fused MODE 0 kernels, 0 = the separate
-    verify + block-decrypt kernels."""
+    verify + block-decrypt kernels, 4 = verify (MODE 6) beside the decrypt of
+    every valid record (MODE 8) on two streams."""
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
     try:
         _eta_variants_decrypt(drv, esn, inplace)
@@ -320,11 +321,11 @@ def test_eta_full_hash_icv_vs_oracle(drv, inplace):
 
 
 def test_eta_fused_knob_range(drv):
-    """eta_fused: 0..3, others EINVAL; the product library serves only the
+    """eta_fused: 0..4, others EINVAL; the product library serves only the
     default 2 (ENOTSUP for the measured-slower designs of the variants build)."""
-    for v in (-1, 4, 7):
+    for v in (-1, 5, 7):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == 22
-    for v in (0, 1, 3):
+    for v in (0, 1, 3, 4):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == (0 if VARIANTS else 95)
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
 
@@ -394,12 +395,12 @@ def test_eta_variants_encrypt_vs_oracle(drv):
         drv.freesession(s)
 
 
-@pytest.mark.parametrize("fused", [2, pytest.param(3, marks=variants_only)])
+@pytest.mark.parametrize("fused", [2, pytest.param(3, marks=variants_only), pytest.param(4, marks=variants_only)])
 def test_eta_variants_trailer(drv, fused):
     """The fused esp_input_cb trailer word for CTR records (partial last
     block) and SHA2-256 sessions, out of place and in place; a record whose
-    ICV fails gets EBADMSG and trailer word 0 (eta_fused 3 decrypts it out of
-    place before its HMAC is known)."""
+    ICV fails gets EBADMSG and trailer word 0 (eta_fused 3 and 4 decrypt it
+    out of place before its HMAC is known)."""
     from espgpu.batch import decrypt_batch
     from espgpu.esp import trailer_word
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
