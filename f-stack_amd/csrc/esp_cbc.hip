@@ -62,6 +62,9 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_HMAC_PREFETCH
 #define ETA_HMAC_PREFETCH 0
 #endif
+#ifndef ETA_LEAN_SHFL
+#define ETA_LEAN_SHFL 1
+#endif
 
 
 constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
@@ -1006,11 +1009,8 @@ __device__ __forceinline__ bool eta_interleaved(const EtaParams &p, const uint8_
 #ifndef ETA_C8_WG
 #define ETA_C8_WG 512
 #endif
-#ifndef ETA_C6_VGPR
-#define ETA_C6_VGPR 512
-#endif
 template <int MODE, int WG, int CKS>
-__device__ __forceinline__ void eta_body(const EtaParams &p) {
+__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
@@ -1301,9 +1301,17 @@ __device__ __forceinline__ void eta_body(const EtaParams &p) {
           fk[k] = f;
           ik[k] = (uint32_t)f - sj;
           rok[k] = __shfl(off, j);
+#if ETA_LEAN_SHFL
+          // (each __shfl is a ds_bpermute on the LDS pipe the AES lookups
+          // bound: only what the session kind uses, wave-uniform conditions)
+          rplk[k] = (ctr || null || p.trailer) ? __shfl(plen, j) : 0u;
+          rdik[k] = p.trailer ? __shfl(di, j) : 0u;
+          rsk[k] = ctr ? __shfl(salt, j) : 0u;
+#else
           rplk[k] = __shfl(plen, j);
           rdik[k] = __shfl(di, j);
           rsk[k] = __shfl(salt, j);
+#endif
         }
         // all loads of the pass before any store (in place: see above)
         uint4 v[U], pv[U];
@@ -1358,16 +1366,6 @@ __device__ __forceinline__ void eta_body(const EtaParams &p) {
   }
 }
 
-template <int MODE, int WG, int CKS>
-__global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
-  eta_body<MODE, WG, CKS>(p);
-}
-// the concurrent design's verify pass, with a register cap so that it fits
-// beside the decrypt waves (eta_fused 4)
-template <int WG>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_num_vgpr(ETA_C6_VGPR))) void eta_verify_kernel(EtaParams p) {
-  eta_body<6, WG, -1>(p);
-}
 
 }  // namespace
 
@@ -1413,6 +1411,7 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     if (in_place) {
       hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+#ifdef ESPGPU_VARIANTS
     } else if (fused == 4 && aux) {
       // concurrent (eta_fused 4, out of place): the verify pass (MODE 6, lane
       // = record SHA-1 / SHA2-256 on the VALU, no LDS) on the aux stream beside
@@ -1426,13 +1425,14 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
       if (hipEventRecord(ef, st) != hipSuccess || hipStreamWaitEvent(sa, ef, 0) != hipSuccess) return -1;
       if (kinds & 3) {
         hipLaunchKernelGGL((eta_kernel<8, ETA_C8_WG, -1>), dim3(clamp(grid, ETA_C8_WG)), dim3(ETA_C8_WG), 0, st, p);
-        hipLaunchKernelGGL((eta_verify_kernel<256>), dim3(clamp(grid, 256)), dim3(256), 0, sa, pv);
+        hipLaunchKernelGGL((eta_kernel<6, 256, -1>), dim3(clamp(grid, 256)), dim3(256), 0, sa, pv);
       }
       if (hipEventRecord(ej, sa) != hipSuccess || hipStreamWaitEvent(st, ej, 0) != hipSuccess) return -1;
       if ((kinds & 3) && p.trailer)
         hipLaunchKernelGGL(eta_trailer_merge, dim3(std::min(1024u, (p.n + 255) / 256)), dim3(256), 0, st, p.status,
                            p.trailer, p.n);
       if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+#endif
     } else if (p.two_pass_all && !p.interleave) {
       hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);

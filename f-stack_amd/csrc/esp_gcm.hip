@@ -1452,15 +1452,11 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0)];
   const int tid = threadIdx.x;
   GCM_PHASE(0, true);
-
-  // T-table: per entry 32 slots of Te0 then 32 slots of Te1 (see tpa()).
-  for (int idx = tid; idx < 256 * 32; idx += WG) {
-    const int x = idx >> 5, r = idx & 31;
-    const uint2 t = p.tpair[x];
-    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
-    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
-  }
-  GCM_PHASE(1, true);
+  // The T-table (per entry 32 slots of Te0 then 32 slots of Te1, see tpa())
+  // is filled with the first session's GHASH table: a workgroup that draws no
+  // chunk (a launch with few GCM chunks, e.g. a batch of ETA records whose
+  // invalid records the GCM kernel marks) leaves without the 64 KiB fill.
+  bool tfilled = false;
 
   const bool implicit = (p.chunks == nullptr);
   const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
@@ -1506,6 +1502,16 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         flags = s->flags;
         mlen = s->mlen;
         mode = s->mode;
+        if (mode == ESPGPU_CSP_MODE_AEAD && !tfilled) {
+          for (int idx = tid; idx < 256 * 32; idx += WG) {
+            const int x = idx >> 5, r = idx & 31;
+            const uint2 t = p.tpair[x];
+            *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
+            *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
+          }
+          tfilled = true;
+          GCM_PHASE(1, true);
+        }
         if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
           const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + gh8);
           uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);

@@ -171,6 +171,8 @@ struct espgpu_ctx {
   // ETA sessions: all, and by kernel: narrow-hash (SHA-1 / SHA2-256) CBC and
   // CTR, wide-hash (SHA2-384/512) CBC and CTR
   int n_eta = 0, n_cbc = 0, n_ctr = 0, n_wcbc = 0, n_wctr = 0;
+  int n_gcm = 0;                 // live AEAD (GCM) sessions
+  bool plan_dirty = true;        // planner key counts not known to be zero (plan_scan re-zeroes them)
   int n_whash = 0;   // ETA sessions with HMAC-SHA2-384/512 (the wide-hash two-pass kernels)
   // ETA decrypt kernels (launch_eta; set_tuning "eta_fused"): 2 (default) =
   // out of place the verify-first two-pass kernel (MODE 3: HMAC lane = record,
@@ -285,6 +287,7 @@ int ensure_plan(espgpu_ctx *c, uint32_t n) {
   HIPCHK(c, hipMalloc(&c->d_order, (size_t)c->plan_cap * 4));
   HIPCHK(c, hipMalloc(&c->d_chunks, (size_t)c->max_chunks * sizeof(Chunk)));
   HIPCHK(c, hipMalloc(&c->d_nchunks, 16));
+  c->plan_dirty = true;
   return 0;
 }
 
@@ -569,9 +572,17 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   if (!(flags & ESPGPU_BATCH_GROUPED)) {
     int e = ensure_plan(c, n);
     if (e) return e;
-    if (launch_plan(d_desc, n, c->d_sas, nsas, c->d_work, c->d_order, c->d_chunks, c->d_nchunks,
-                    c->max_chunks, st))
+    // the key counts start at zero: plan_scan zeroes them after reading, so
+    // only a fresh workspace (or one a failed launch left behind) needs it
+    if (c->plan_dirty) {
+      HIPCHK(c, hipMemsetAsync(c->d_work, 0, plan_workspace_words(c->cfg.max_sessions) * 4, st));
+      c->plan_dirty = false;
+    }
+    if (launch_plan(d_desc, n, c->d_sas, nsas, c->cfg.max_sessions, c->d_work, c->d_order, c->d_chunks, c->d_nchunks,
+                    c->max_chunks, st)) {
+      c->plan_dirty = true;
       return fail(c, ESPGPU_ENOTSUP, "planner: too many sessions for device grouping (%u); pre-group and pass ESPGPU_BATCH_GROUPED", nsas);
+    }
     p.order = c->d_order;
     p.chunks = c->d_chunks;
     p.nchunks = c->d_nchunks;
@@ -599,7 +610,12 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   // run for the launch to finish
   int grid = c->cfg.grid ? (int)c->cfg.grid : 256;
   if (c->door_live && !door_exited(c)) grid = std::max(1, grid - c->door_wg);
-  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, grid, c->gcm_lanes, st, &bs))
+  // A context without GCM sessions still launches the GCM kernel for the
+  // records whose session is invalid (EINVAL; the planner chunks them with the
+  // GCM records), but a few workgroups do: the others would only draw a
+  // ticket past the end (cfg3: ~9 us -> ~3 us per batch)
+  const int ggrid = c->n_gcm > 0 ? grid : std::min(grid, 16);
+  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, ggrid, c->gcm_lanes, st, &bs))
     return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if ((kinds & 2) && c->n_eta > 0) {
     EtaParams q{};
@@ -890,6 +906,8 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     c->n_eta++;
     eta_count(c, s)++;
     c->n_whash += s.whash ? 1 : 0;
+  } else {
+    c->n_gcm++;
   }
   c->h_sas[slot] = sa;
   *sid_out = slot;
@@ -917,6 +935,8 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
     c->n_eta--;
     eta_count(c, fs)--;
     c->n_whash -= fs.whash ? 1 : 0;
+  } else {
+    c->n_gcm--;
   }
   c->sessions[sid] = Session();
   DevSA z;

@@ -238,7 +238,7 @@ int launch_replay_check(const uint8_t *arena, espgpu_desc *desc, uint32_t n, con
                         uint32_t nrp, const uint32_t *bitmap, uint8_t *rstatus, void *stream);
 int launch_xfer(const XferSpan *spans, uint32_t nspans, const uint8_t *status, void *stream);
 int launch_replay_merge(uint8_t *status, const uint8_t *rstatus, uint32_t n, void *stream);
-int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
+int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas, uint32_t cap_sas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream);
 size_t plan_workspace_words(uint32_t nsas);

@@ -1,11 +1,13 @@
 // plan.hip — device-side batch planner: groups ESP records by (size class,
 // session) so that each 256-record chunk of the GCM kernel has ONE session
 // (its GHASH power tables and round keys are staged once in LDS) and records
-// of similar length share a wave.  Three small kernels, no host round trip:
+// of similar length share a wave.  Four small kernels, no host round trip:
 //   plan_count   per-workgroup LDS histogram of keys, flushed with one global
 //                atomic per non-empty key per workgroup
 //   plan_scan    one workgroup: exclusive scan of key counts -> record offsets
-//                and chunk offsets; writes the chunk list and its length
+//                and chunk offsets per key, the chunk count; zeroes the counts
+//   plan_emit    the chunk list, one chunk per thread (binary search of the
+//                per-key chunk offsets in LDS)
 //   plan_scatter per-workgroup LDS ranks + one global range reservation per
 //                non-empty key -> order[] (a permutation of descriptor ids)
 // Keys: [0, 4*nsas) = GCM records (class-major, largest class first),
@@ -67,28 +69,32 @@ __global__ __launch_bounds__(PWG) void plan_count(const espgpu_desc *desc, uint3
     if (hist[k]) atomicAdd(&gcnt[k], hist[k]);
 }
 
-// Single workgroup.  gcnt[nkeys] -> gcur[nkeys] (record cursor), chunks.
-// Scan of the per-key record and chunk counts (each thread sums a run of
-// keys, Hillis-Steele over the 1024 partials), per-key offsets into LDS,
-// then every thread emits chunks c = tid, tid + 1024, ...: the key of chunk c
-// is the last key whose first chunk is <= c (binary search in LDS), so the
-// chunk list is written evenly by all threads whatever the key sizes.  (The
-// kernel takes ~33 us for 1K ETA sessions either way; the serial per-thread
-// emission it replaced was not its cost.)
-__global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t nsas,
-                                                 uint32_t *gcur, Chunk *chunks,
-                                                 uint32_t *nchunks, uint32_t max_chunks) {
+// Single workgroup.  gcnt[nkeys] -> gcur[nkeys] (record cursor), and the
+// per-key first record and first chunk (groff / gcoff, nkeys + 1 entries)
+// that plan_emit turns into the chunk list.  Scan of the per-key record and
+// chunk counts: each thread sums a run of keys, Hillis-Steele over the 1024
+// partials.
+__global__ __launch_bounds__(PWG) void plan_scan(uint32_t *gcnt, uint32_t nsas, uint32_t *gcur,
+                                                 uint32_t *groff, uint32_t *gcoff, uint32_t *nchunks,
+                                                 uint32_t max_chunks) {
   __shared__ uint32_t s_rec[PWG], s_chk[PWG];
-  // per key: first chunk, first record (s_roff[nkeys] = all records)
-  __shared__ uint32_t s_coff[kMaxLdsKeys], s_roff[kMaxLdsKeys + 1];
+  __shared__ uint32_t s_cnt[kMaxLdsKeys];
   const uint32_t nkeys = num_keys(nsas);
   const uint32_t per = (nkeys + PWG - 1) / PWG;
   const uint32_t k0 = threadIdx.x * per, k1 = min(nkeys, k0 + per);
   const uint32_t eta0 = 4 * nsas + 1;                       // first ETA key
   auto recs_per_chunk = [&](uint32_t k) { return k >= eta0 ? 64u : (uint32_t)kChunkRecs; };
+  // The counts into LDS with coalesced, independent loads (a thread's run of
+  // keys read from global memory one dependent load after another was most
+  // of this kernel's time), then zeroed for the next plan: each thread clears
+  // what it loaded, so plan_count of the next batch starts from zero with no
+  // memset (the workspace's whole key capacity is zero between plans).
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) s_cnt[k] = gcnt[k];
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) gcnt[k] = 0;
   uint32_t r = 0, c = 0;
   for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t cnt = gcnt[k];
+    const uint32_t cnt = s_cnt[k];
     r += cnt;
     c += (cnt + recs_per_chunk(k) - 1) / recs_per_chunk(k);
   }
@@ -105,40 +111,59 @@ __global__ __launch_bounds__(PWG) void plan_scan(const uint32_t *gcnt, uint32_t 
   }
   uint32_t roff = s_rec[threadIdx.x] - r, coff = s_chk[threadIdx.x] - c;
   for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t cnt = gcnt[k];
+    const uint32_t cnt = s_cnt[k];
     gcur[k] = roff;                       // record cursor (plan_scatter) = the key's first record
-    s_roff[k] = roff;
-    s_coff[k] = coff;
+    groff[k] = roff;
+    gcoff[k] = coff;
+    // the GCM kernel's share: the chunks before the first ETA key
+    if (k == eta0) nchunks[0] = min(coff, max_chunks);
     roff += cnt;
     coff += (cnt + recs_per_chunk(k) - 1) / recs_per_chunk(k);
   }
-  if (threadIdx.x == PWG - 1) s_roff[nkeys] = s_rec[PWG - 1];
-  __syncthreads();
-  const uint32_t total = s_chk[PWG - 1];
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == PWG - 1) {
+    const uint32_t total = s_chk[PWG - 1];
+    groff[nkeys] = s_rec[PWG - 1];
+    gcoff[nkeys] = total;
     nchunks[1] = min(total, max_chunks);
-    // the GCM kernel's share: the chunks before the first ETA key
-    nchunks[0] = eta0 < nkeys ? min(s_coff[eta0], max_chunks) : nchunks[1];
+    if (eta0 >= nkeys) nchunks[0] = min(total, max_chunks);   // no ETA keys (no sessions)
   }
-  const uint32_t lim = min(total, max_chunks);
-  for (uint32_t ci = threadIdx.x; ci < lim; ci += PWG) {
-    uint32_t lo = 0, hi = nkeys;                          // last key with s_coff <= ci
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_coff[mid] <= ci) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t k = lo, cnt = s_roff[k + 1] - s_roff[k], rpc = recs_per_chunk(k);
-    const uint32_t sa = k == 4 * nsas ? 0xffffffffu : (k >= eta0 ? k - eta0 : k % nsas);
-    const uint32_t cls = k >= 4 * nsas ? 4u : 3u - k / nsas;
-    // ceil(cnt / rpc) chunks of EQUAL size (270 records -> 135 + 135, not
-    // 256 + 14): a workgroup's pass time grows with its busy waves, so a
-    // near-empty remainder chunk costs almost a full pass (cfg2: 1K sessions
-    // x 4 size classes leave ~256 +- 16 records per key)
-    const uint32_t nc = (cnt + rpc - 1) / rpc, jj = ci - s_coff[k];
-    const uint32_t a = (uint32_t)((uint64_t)cnt * jj / nc), b = (uint32_t)((uint64_t)cnt * (jj + 1) / nc);
-    chunks[ci] = Chunk{sa, s_roff[k] + a, b - a, cls};
+}
+
+// The chunk list, written by every thread of ceil(max_chunks / PWG)
+// workgroups (one workgroup emitting ~16K ETA chunks by binary search was
+// most of the planner's time): chunk c belongs to the last key whose first
+// chunk is <= c (binary search over the per-key offsets, staged in LDS).
+__global__ __launch_bounds__(PWG) void plan_emit(uint32_t nsas, const uint32_t *groff, const uint32_t *gcoff,
+                                                 Chunk *chunks, const uint32_t *nchunks) {
+  __shared__ uint32_t s_coff[kMaxLdsKeys + 1], s_roff[kMaxLdsKeys + 1];
+  const uint32_t lim = nchunks[1];
+  const uint32_t c0 = blockIdx.x * PWG;
+  if (c0 >= lim) return;                                  // workgroup-uniform
+  const uint32_t nkeys = num_keys(nsas);
+  const uint32_t eta0 = 4 * nsas + 1;
+  for (uint32_t k = threadIdx.x; k <= nkeys; k += PWG) {
+    s_coff[k] = gcoff[k];
+    s_roff[k] = groff[k];
   }
+  __syncthreads();
+  const uint32_t ci = c0 + threadIdx.x;
+  if (ci >= lim) return;
+  uint32_t lo = 0, hi = nkeys;                            // last key with s_coff <= ci
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s_coff[mid] <= ci) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t k = lo, cnt = s_roff[k + 1] - s_roff[k], rpc = k >= eta0 ? 64u : (uint32_t)kChunkRecs;
+  const uint32_t sa = k == 4 * nsas ? 0xffffffffu : (k >= eta0 ? k - eta0 : k % nsas);
+  const uint32_t cls = k >= 4 * nsas ? 4u : 3u - k / nsas;
+  // ceil(cnt / rpc) chunks of EQUAL size (270 records -> 135 + 135, not
+  // 256 + 14): a workgroup's pass time grows with its busy waves, so a
+  // near-empty remainder chunk costs almost a full pass (cfg2: 1K sessions
+  // x 4 size classes leave ~256 +- 16 records per key)
+  const uint32_t nc = (cnt + rpc - 1) / rpc, jj = ci - s_coff[k];
+  const uint32_t a = (uint32_t)((uint64_t)cnt * jj / nc), b = (uint32_t)((uint64_t)cnt * (jj + 1) / nc);
+  chunks[ci] = Chunk{sa, s_roff[k] + a, b - a, cls};
 }
 
 __global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uint32_t n,
@@ -172,22 +197,27 @@ __global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uin
 
 }  // namespace
 
-// gcnt[nkeys] + gcur[nkeys]
-size_t plan_workspace_words(uint32_t nsas) { return 2 * (size_t)num_keys(nsas); }
+// gcnt, gcur: one word per key; groff, gcoff: one more (the totals)
+size_t plan_workspace_words(uint32_t nsas) { return 4 * (size_t)num_keys(nsas) + 2; }
 uint32_t plan_max_chunks(uint32_t n, uint32_t nsas) { return n / 64 + num_keys(nsas) + 8; }
 
-int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas,
+int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_t nsas, uint32_t cap_sas,
                 uint32_t *d_work, uint32_t *d_order, Chunk *d_chunks, uint32_t *d_nchunks,
                 uint32_t max_chunks, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const uint32_t nkeys = num_keys(nsas);
-  if (nkeys > kMaxLdsKeys) return -1;     // caller must pre-group (ESPGPU_BATCH_GROUPED)
-  uint32_t *gcnt = d_work, *gcur = d_work + nkeys;
-  if (hipMemsetAsync(gcnt, 0, nkeys * sizeof(uint32_t), st) != hipSuccess) return -1;
+  if (nkeys > kMaxLdsKeys || nsas > cap_sas) return -1;   // caller must pre-group (ESPGPU_BATCH_GROUPED)
+  // gcnt is zero on entry (plan_scan re-zeroes it) over the workspace's whole
+  // key capacity; the cursors sit after that capacity, not after this batch's
+  // keys: the key count grows with the session table, and cursor words left
+  // where a later batch's counts go would be counted
+  const uint32_t capk = num_keys(cap_sas);
+  uint32_t *gcnt = d_work, *gcur = d_work + capk, *groff = gcur + capk, *gcoff = groff + capk + 1;
   const uint32_t grid = (n + TILE - 1) / TILE;
   if (grid) hipLaunchKernelGGL(plan_count, dim3(grid), dim3(PWG), 0, st, d_desc, n, sas, nsas, gcnt);
-  hipLaunchKernelGGL(plan_scan, dim3(1), dim3(PWG), 0, st, gcnt, nsas, gcur, d_chunks, d_nchunks,
-                     max_chunks);
+  hipLaunchKernelGGL(plan_scan, dim3(1), dim3(PWG), 0, st, gcnt, nsas, gcur, groff, gcoff, d_nchunks, max_chunks);
+  hipLaunchKernelGGL(plan_emit, dim3((max_chunks + PWG - 1) / PWG), dim3(PWG), 0, st, nsas, groff, gcoff, d_chunks,
+                     d_nchunks);
   if (grid) hipLaunchKernelGGL(plan_scatter, dim3(grid), dim3(PWG), 0, st, d_desc, n, sas, nsas, gcur,
                                d_order);
   return hipGetLastError() == hipSuccess ? 0 : -1;

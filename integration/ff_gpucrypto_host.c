@@ -17,6 +17,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "espgpu.h"
 
@@ -53,17 +54,27 @@ int ff_gpucrypto_host_init(int gpu)
 }
 
 /* ff_init(): F-Stack process proc_id (one lcore) opens device
- * proc_id mod (visible devices), the SPI-sharded layout of INTEGRATION.md
- * section 6 with one process per GPU. */
+ * proc_id mod (visible devices): the GPUs are split by lcore, i.e. by the RSS
+ * queues NIC steers to each lcore.
+ * FF_GPUCRYPTO_DOOR=N (1..256) starts the doorbell path on N CUs: bursts are
+ * handed to a resident kernel through pinned host memory instead of a launch
+ * each (a 32-record burst 42 -> 25 us).  Off by default:
+ * the resident kernel keeps N CUs while bursts arrive (it exits after 20 ms
+ * without one). */
 int ff_gpucrypto_host_init_proc(int proc_id)
 {
 	int n = espgpu_device_count(), e;
+	const char *door;
 
 	if (n <= 0)
 		return ESPGPU_ENODEV;
 	e = ff_gpucrypto_host_init(proc_id % n);
-	if (e == ESPGPU_OK)
+	if (e == ESPGPU_OK) {
 		ff_gpucrypto_host_set_noqueue(1);
+		door = getenv("FF_GPUCRYPTO_DOOR");
+		if (door && atoi(door) > 0)
+			espgpu_set_tuning(g_ctx, "door", atoi(door));
+	}
 	return e;
 }
 

@@ -26,6 +26,7 @@
 
 extern const struct kmock_cryptodev ff_gpucrypto_kmock;
 int  ff_gpucrypto_host_configure(const struct espgpu_config *c);
+int  ff_gpucrypto_host_init_proc(int proc_id);
 void ff_gpucrypto_host_set_noqueue(int on);
 void ff_gpucrypto_host_fini(void);
 int  ff_gpucrypto_host_register(void *base, uint64_t len);
@@ -66,6 +67,18 @@ kd_open(int batch_records, int nbatches, int batch_bytes, int noqueue)
 		return (e);
 	ff_gpucrypto_host_set_noqueue(noqueue);
 	return (0);
+}
+
+/* as ff_init() opens it: ff_gpucrypto_host_init_proc (device proc_id mod
+ * n, F-Stack mode, FF_GPUCRYPTO_DOOR from the environment), then attach */
+int
+kd_open_proc(int proc_id)
+{
+	int e;
+
+	if ((e = ff_gpucrypto_host_init_proc(proc_id)) != 0)
+		return (e);
+	return (kmock_attach(&ff_gpucrypto_kmock));
 }
 
 void
@@ -204,12 +217,13 @@ kd_counters(int *out4)
 
 /* engine counters: zero-copy records, overflow entries */
 void
-kd_engine(uint64_t *out2)
+kd_engine(uint64_t *out3)
 {
 	struct espgpu_stats s;
 
 	memset(&s, 0, sizeof(s));
 	ff_gpucrypto_host_stats(&s);
-	out2[0] = s.zerocopy;
-	out2[1] = s.overflow;
+	out3[0] = s.zerocopy;
+	out3[1] = s.overflow;
+	out3[2] = s.door;
 }

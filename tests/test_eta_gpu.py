@@ -684,3 +684,50 @@ def test_eta_mixed_sessions_in_one_wave_unit(drv, fused):
         assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
         for s in sids:
             drv.freesession(s)
+
+
+def test_planner_as_the_session_table_grows():
+    """Planner batches while the session table grows between them (the key
+    count is 5 x sessions + 1, so each batch's key range is larger than the
+    last): the per-key counts a batch starts from must be zero over the whole
+    range, whatever the earlier batches left in the workspace.  GCM and ETA
+    sessions added in rounds of 1, 4, 16 and 40, a batch over all sessions so
+    far after each round: statuses and plaintext vs the oracle."""
+    from espgpu.batch import decrypt_batch
+    from espgpu.opencrypto import GpuCryptoDriver
+    d = GpuCryptoDriver(max_sessions=128)
+    try:
+        rng = np.random.default_rng(1700)
+        sas, sids = [], []
+        for grow in (1, 4, 16, 40):
+            new = [GcmSA(rng, 16) if rng.random() < 0.5 else EtaSA(rng, 16, sha256=bool(rng.random() < 0.5))
+                   for _ in range(grow)]
+            sids += _sessions(d, new)
+            sas += new
+            n = 200 + 10 * len(sas)
+            sa_idx = rng.integers(0, len(sas), n)
+            cts = np.where([isinstance(sas[i], GcmSA) for i in sa_idx], rng.integers(1, 90, n) * 16 - 4,
+                           rng.integers(1, 90, n) * 16)
+            eh = np.zeros(n, dtype=np.uint32)
+            plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, esn_hi=eh)
+            bad = ct.copy()
+            flip = rng.random(n) < 0.1
+            for i in np.nonzero(flip)[0]:
+                o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+                bad[o + L - 1] ^= 0x01                          # inside the ICV
+            ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+            dd = descs.copy()
+            dd["sa"] = [sids[s] for s in sa_idx]
+            arena = _dev(bad)
+            out = torch.zeros_like(arena)
+            st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+            decrypt_batch(d, arena, _descs_dev(dd), n, st, out=out, grouped=False)
+            torch.cuda.synchronize()
+            got = st.cpu().numpy()
+            assert (got == ref_st).all(), (len(sas), np.nonzero(got != ref_st)[0][:10])
+            hl, ml = _hl(sas, sa_idx)
+            ok = got == 0
+            m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
+            assert (out.cpu().numpy()[m_ok] == ref_out[m_ok]).all()
+    finally:
+        d.close()

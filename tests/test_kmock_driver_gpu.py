@@ -58,7 +58,7 @@ class _Fw:
 class KmockDriver:
     """ff_gpucrypto.c over the kmock KPI, host shim, libespgpu.so."""
 
-    def __init__(self, batch_records=64, nbatches=2, batch_bytes=4 << 20, noqueue=True):
+    def __init__(self, batch_records=64, nbatches=2, batch_bytes=4 << 20, noqueue=True, proc_id=None):
         if not torch.cuda.is_available():
             pytest.fail("GPU test run without a visible HIP device")
         L = C.CDLL(KD_LIB)
@@ -73,7 +73,10 @@ class KmockDriver:
         L.kd_free.argtypes = [vp]
         L.kd_register.argtypes = [vp, C.c_uint64]
         self.L = L
-        rc = L.kd_open(batch_records, nbatches, batch_bytes, int(noqueue))
+        if proc_id is not None:               # as ff_init() opens it (ff_gpucrypto_host_init_proc)
+            rc = L.kd_open_proc(proc_id)
+        else:
+            rc = L.kd_open(batch_records, nbatches, batch_bytes, int(noqueue))
         assert rc == 0, rc
         self._keep = []
 
@@ -133,9 +136,9 @@ class KmockDriver:
         return dict(zip(("erestarts", "queued", "blocked", "done"), list(a)))
 
     def engine(self):
-        a = (C.c_uint64 * 2)()
+        a = (C.c_uint64 * 3)()
         self.L.kd_engine(a)
-        return dict(zip(("zerocopy", "overflow"), list(a)))
+        return dict(zip(("zerocopy", "overflow", "door"), list(a)))
 
     def free(self, reqs):
         for r in reqs:
@@ -490,6 +493,60 @@ def test_registered_memory_through_kernel_driver_vs_oracle(kd):
             assert region[base + h:base + L - a].tobytes() == plain[o + h:o + L - a].tobytes(), i
     for h in ses:
         kd.freesession(h)
+
+
+def test_doorbell_through_kernel_driver_vs_oracle(monkeypatch):
+    """F-Stack's init path with FF_GPUCRYPTO_DOOR set
+    (ff_gpucrypto_host_init_proc): 32-packet GCM bursts from registered mbuf
+    memory go to the resident doorbell kernel (door count), encrypt equals the
+    oracle's ciphertext, a tampered decrypt the oracle's statuses and
+    plaintext, failed packets untouched."""
+    from espgpu.esp import esp_input_crp, esp_output_crp
+    monkeypatch.setenv("FF_GPUCRYPTO_DOOR", "16")
+    kd = KmockDriver(proc_id=0)
+    try:
+        rng = np.random.default_rng(4500)
+        sa = GcmSA(rng, 16)
+        n, slot = 32, 2048
+        idx = np.zeros(n, dtype=np.int64)
+        cts = rng.integers(1, 90, n) * 16
+        plain, ct, descs, eh = build_records(rng, [sa], idx, cts)
+        region = np.zeros(n * slot, dtype=np.uint8)
+        mv = memoryview(region)
+        e, ses = kd.newsession(sa.esp_sa())
+        assert e == 0
+        assert kd.L.kd_register(region.ctypes.data, region.nbytes) == 0
+        views = [mv[i * slot + 162:i * slot + 182 + int(descs["len"][i])] for i in range(n)]
+        for i in range(n):
+            region[i * slot + 162:i * slot + 182 + int(descs["len"][i])] = np.frombuffer(_pkt(plain, descs, i), np.uint8)
+        d0 = kd.engine()["door"]
+        reqs = [_req_view(kd, esp_output_crp, ses, sa.esp_sa(), v) for v in views]
+        assert kd.wait(reqs) == [0] * n
+        kd.free(reqs)
+        for i in range(n):
+            L = int(descs["len"][i])
+            assert region[i * slot + 182:i * slot + 182 + L].tobytes() == _pkt(ct, descs, i)[20:], i
+        flip = rng.random(n) < 0.25
+        for i in np.flatnonzero(flip):
+            region[i * slot + 182 + int(descs["len"][i]) - 1] ^= 0x02
+        before = region.copy()
+        reqs = [_req_view(kd, esp_input_crp, ses, sa.esp_sa(), v) for v in views]
+        ets = kd.wait(reqs)
+        kd.free(reqs)
+        assert kd.engine()["door"] > d0
+        for i in range(n):
+            L, h, a = int(descs["len"][i]), sa.hlen, sa.mlen
+            base = i * slot + 182
+            o = int(descs["off4"][i]) * 4
+            if flip[i]:
+                assert ets[i] == BSD_EBADMSG
+                assert (region[base:base + L] == before[base:base + L]).all()
+            else:
+                assert ets[i] == 0
+                assert region[base + h:base + L - a].tobytes() == plain[o + h:o + L - a].tobytes(), i
+        kd.freesession(ses)
+    finally:
+        kd.close()
 
 
 def _req_view(kd, build, ses, esa, view):
