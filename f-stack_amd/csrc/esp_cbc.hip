@@ -65,6 +65,9 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_LEAN_SHFL
 #define ETA_LEAN_SHFL 1
 #endif
+#ifndef ETA_LANE_MAP
+#define ETA_LANE_MAP 0
+#endif
 
 
 constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
@@ -1290,6 +1293,44 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           // the record holding flat block f: the last lane whose start <= f
           int j = 0;
           uint32_t sj = 0;
+#if ETA_LANE_MAP
+          // The pass's 64 blocks of this k are one window [F, F + 63]: the
+          // record of its first block from a ballot (no LDS), and when at
+          // most three more records start inside the window (records of >= 22
+          // blocks; ties of lanes without blocks included) each lane's record
+          // is one of four, read with v_readlane: no ds_bpermute for the
+          // search or the record's offset (they share the LDS pipe with the
+          // AES lookups).  Otherwise the shuffle search below.
+          const int F = base + 64 * k, Fc = F < 0 ? 0 : F;
+          const int j0 = (int)__builtin_popcountll(__ballot((int)start <= Fc)) - 1;
+          auto rl = [&](uint32_t v, int jj) { return (uint32_t)__builtin_amdgcn_readlane((int)v, jj > 63 ? 63 : jj); };
+          const int s1 = j0 + 1 > 63 ? INT32_MAX : (int)rl(start, j0 + 1);
+          const int s2 = j0 + 2 > 63 ? INT32_MAX : (int)rl(start, j0 + 2);
+          const int s3 = j0 + 3 > 63 ? INT32_MAX : (int)rl(start, j0 + 3);
+          const int s4 = j0 + 4 > 63 ? INT32_MAX : (int)rl(start, j0 + 4);
+          const bool fast = s4 > F + 63;                              // wave-uniform
+          int m = 0;
+          if (fast) {
+            m = (f >= s1) + (f >= s2) + (f >= s3);
+            j = j0 + m;
+            const uint32_t st0 = rl(start, j0);
+            sj = m == 0 ? st0 : (m == 1 ? (uint32_t)s1 : (m == 2 ? (uint32_t)s2 : (uint32_t)s3));
+            const uint32_t o0 = rl(off, j0), o1 = rl(off, j0 + 1), o2 = rl(off, j0 + 2), o3 = rl(off, j0 + 3);
+            rok[k] = m == 0 ? o0 : (m == 1 ? o1 : (m == 2 ? o2 : o3));
+          } else {
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+              const uint32_t sc = __shfl(start, j + step);
+              if ((int)sc <= f) {
+                j += step;
+                sj = sc;
+              }
+            }
+            rok[k] = __shfl(off, j);
+          }
+          fk[k] = f;
+          ik[k] = (uint32_t)f - sj;
+#else
 #pragma unroll
           for (int step = 32; step >= 1; step >>= 1) {
             const uint32_t sc = __shfl(start, j + step);
@@ -1301,6 +1342,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           fk[k] = f;
           ik[k] = (uint32_t)f - sj;
           rok[k] = __shfl(off, j);
+#endif
 #if ETA_LEAN_SHFL
           // (each __shfl is a ds_bpermute on the LDS pipe the AES lookups
           // bound: only what the session kind uses, wave-uniform conditions)

@@ -163,3 +163,23 @@ def test_cfg4_rank_of_8_spi_shard(drv, rank):
     _check_decrypt(drv, sids, sa_idx, descs, bad, flip, ref_out, ref_st, plain, 16, 16)
     for s in sids:
         drv.freesession(int(s))
+
+
+def test_planner_runs_of_one_session(drv):
+    """Planner batch whose sessions hold hundreds of chunks each (4 GCM SAs x
+    ~200K records of two size classes): the GCM kernel draws runs of chunks
+    of one session at a time (GCM_GROUP) except in the queue's last 2 x grid
+    chunks; every record against the oracle, out of place and in place."""
+    rng = np.random.default_rng(0xC5)
+    nsa, n = 4, 800_000
+    sas = [GcmSA(rng, 16) for _ in range(nsa)]
+    sids = _sessions(drv, sas)
+    sa_idx = rng.integers(0, nsa, n)
+    cts = rng.choice([12, 204], n)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts)
+    bad, flip = _flip_icvs(rng, ct, descs, 0.01, 16)
+    ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+    _check_decrypt(drv, sids, sa_idx, descs, bad, flip, ref_out, ref_st, plain, 16, 16)
+    for s in sids:
+        drv.freesession(int(s))
