@@ -1352,7 +1352,9 @@ static int complete_slot(espgpu_ctx *c, Slot &s) {
 
 int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
   if (!c) return -ESPGPU_EINVAL;
-  // completions of flushed batches, oldest first
+  // completions of flushed batches, oldest first, and in arrival order: a
+  // batch that finished before an older one (another stream's kernel, a
+  // doorbell job another workgroup took) waits for it
   bool door_wait = false;
   const uint64_t now = c->door_ctl ? now_ns() : 0;
   for (size_t k = 0; k < c->slots.size(); ++k) {
@@ -1361,12 +1363,12 @@ int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
     if (s.door_job >= 0) {
       if (!door_done(c, s.door_job)) {
         // outstanding for over 1 ms: make sure the kernel is still there
-        door_wait |= now - s.door_t0 > 1000000u;
-        continue;
+        door_wait = now - s.door_t0 > 1000000u;
+        break;
       }
       s.door_job = -1;
     } else if (hipEventQuery(s.done) != hipSuccess) {
-      continue;
+      break;
     }
     complete_slot(c, s);
   }
