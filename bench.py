@@ -2,7 +2,11 @@
 """Benchmark: device-resident ESP AES-128-GCM decrypt, 1M x 1500-B packets per GPU.
 
 One step = one pass of the hot path (verify + decrypt) over one batch of
-1,048,576 ESP records already resident in HBM (BASELINE.json configs[1]).
+1,048,576 ESP records already resident in HBM (BASELINE.json configs[1]),
+decrypted in place with verify-first semantics as F-Stack's opencrypto
+consumer asks (esp_input: CRYPTO_BUF_MBUF in place, cryptosoft.c:595-633);
+step k works on its own copy of the ciphertext, so no restore copy is timed.
+--out-of-place times the single-pass out-of-place decrypt instead.
 N GPUs = N processes (torchrun), each with its own SAs chosen so that
 fnv1_32(spi) mod N == rank (SPI-hash sharding, no collective on the data path);
 per-GPU work is fixed (weak scaling) and value = all ranks' bytes / max time.
@@ -124,10 +128,13 @@ def main():
                     help="0 = every core of this process's CPU share (affinity and cgroup quota)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="cpu_baseline: median of this many runs")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inplace", action="store_true",
-                    help="time the verify-first in-place decrypt as the headline (default: out of place, "
-                         "with the in-place rate reported beside it)")
-    ap.add_argument("--no-inplace-leg", action="store_true", help="skip the in-place side measurement")
+    ap.add_argument("--out-of-place", action="store_true",
+                    help="time the out-of-place single-pass decrypt as the headline (default: the "
+                         "verify-first in-place decrypt, the opencrypto contract, with the out-of-place "
+                         "rate reported beside it)")
+    ap.add_argument("--inplace", action="store_true", help="the default headline mode (kept for old scripts)")
+    ap.add_argument("--no-inplace-leg", action="store_true",
+                    help="skip the side measurement of the other decrypt mode")
     ap.add_argument("--no-encrypt-leg", action="store_true", help="skip the encrypt-direction side measurement")
     ap.add_argument("--no-packed-leg", action="store_true",
                     help="skip the packed-output side measurement (espgpu_decrypt_batch_packed)")
@@ -140,6 +147,7 @@ def main():
     ap.add_argument("--out-pad", type=int, default=0,
                     help="experiment: extra bytes per record in the out-of-place buffer (layout probes)")
     args = ap.parse_args()
+    inplace = not args.out_of_place
 
     import torch
     import torch.distributed as dist
@@ -204,8 +212,18 @@ def main():
     encrypt_batch(drv, arena, desc, n, status, grouped=grouped)     # build valid ESP records (untimed)
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0, "record generation failed"
-    out = None if args.inplace else torch.empty(total + args.out_pad * n, dtype=torch.uint8, device=dev)
-    pristine = arena.clone() if args.inplace else None
+    out = None if inplace else torch.empty(total + args.out_pad * n, dtype=torch.uint8, device=dev)
+    # In place, every timed step needs ciphertext: step k decrypts its own copy
+    # of the records (`arena` itself stays ciphertext for the side legs), as
+    # many copies as K steps when HBM holds them (288 GB: 20 x 1.5 GB), else
+    # timed segments of as many steps with the copies restored between them,
+    # outside the timed region.  Each copy is cold (1.5 GB >> L2 + MALL).
+    if inplace:
+        free = torch.cuda.mem_get_info(dev)[0]
+        ncopy = max(1, min(args.steps, int(free * 0.6) // total))
+        bufs = [arena.clone() for _ in range(ncopy)]
+    else:
+        bufs = [arena]
     rec_bytes = int(d["len"].astype(np.int64).sum())
     pkt_bytes = int(sizes.astype(np.int64).sum())
     ct_bytes = rec_bytes - HDR_TRAILER[cfg["alg"]] * n
@@ -214,32 +232,48 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-    def step():
-        if pristine is not None:
-            arena.copy_(pristine)
-        decrypt_batch(drv, arena, desc, n, status, out=out, grouped=grouped, stream=stream)
+    def step(k):
+        decrypt_batch(drv, bufs[k % len(bufs)], desc, n, status, out=out, grouped=grouped, stream=stream)
+
+    def restore():
+        if inplace:
+            with torch.cuda.stream(stream):
+                for b in bufs:
+                    b.copy_(arena)
+        torch.cuda.synchronize()
 
     with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step()
+        for k in range(args.warmup):
+            if inplace:
+                bufs[0].copy_(arena)
+            step(0)
+        if inplace:
+            bufs[0].copy_(arena)
     torch.cuda.synchronize()
     knobs = any(kv.split("=")[0] in ("gcm_opts", "eta_opts") and not kv.endswith("=0") for kv in args.tuning)
     assert knobs or int((status != 0).sum()) == 0, "decrypt/verify failed"   # knobs break results on purpose
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        ev0.record(stream)
-        for _ in range(args.steps):
-            step()
-        ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    dt = t1 - t0
-    ev_ms = ev0.elapsed_time(ev1)
+    dt, ev_ms, done = 0.0, 0.0, 0
+    while done < args.steps:
+        seg = min(len(bufs), args.steps - done)
+        if done:
+            restore()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            ev0.record(stream)
+            for k in range(seg):
+                step(k)
+            ev1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt += time.perf_counter() - t0
+        ev_ms += ev0.elapsed_time(ev1)
+        done += seg
+    assert knobs or int((status != 0).sum()) == 0, "decrypt/verify failed in the timed steps"
+    del bufs
     dt, all_pkt_bytes = aggregate(dist, world, dt, pkt_bytes, dev)
     ms_per_step = dt * 1e3 / args.steps
     value = all_pkt_bytes * args.steps / dt / 1e9
@@ -254,7 +288,8 @@ def main():
         "config": {"workload": cfg["workload"], "packets_per_gpu": n, "packet_bytes": pkt_bytes // n,
                    "esp_record_bytes": rec_bytes // n, "sas_per_gpu": len(spis),
                    "sharding": "fnv1_32(spi) mod n_gpus (key_u32hash, key.c:295)",
-                   "decrypt": "in-place verify-first" if args.inplace else "out-of-place single pass",
+                   "decrypt": ("in place, verify first (the opencrypto contract, cryptosoft.c:595-633)"
+                               if inplace else "out-of-place single pass"),
                    "value_bytes": "whole packet bytes incl. outer IPv4 header (BASELINE.json metric)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -273,28 +308,31 @@ def main():
         log("hbm copy measurement skipped: %s" % e)
     if world > 1:
         result["config"]["packets_per_rank"] = per_rank(dist, world, rank, n, dev)
-    kernel = launched_kernel(cfg, args.inplace)
+    if inplace:
+        result["config"]["inplace_copies"] = ncopy
+    kernel = launched_kernel(cfg, inplace)
     result["roofline"]["kernel"] = kernel
-    result["roofline"].update(profile_traffic(args.config, args.inplace, kernel, kern_ms))
-    if not args.inplace and not args.no_inplace_leg:
-        result["inplace"] = inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes,
-                                        algo_bytes, world, dist, launched_kernel(cfg, True))
+    result["roofline"].update(profile_traffic(args.config, inplace, kernel, kern_ms))
+    if not args.no_inplace_leg:
+        leg = side_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes,
+                       algo_bytes, world, dist, launched_kernel(cfg, not inplace), not inplace)
+        result["inplace" if not inplace else "out_of_place"] = leg
 
-    if not args.inplace and not args.no_packed_leg and cfg["alg"] == "gcm":
+    if not args.no_packed_leg and cfg["alg"] == "gcm":
         result["packed_out"] = packed_leg(drv, arena, desc, d, n, status, grouped, stream, pkt_bytes,
                                           algo_bytes, world, dist)
 
-    if not args.inplace and not args.no_encrypt_leg:
+    if not args.no_encrypt_leg:
         result["encrypt"] = encrypt_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, world, dist, cfg)
 
     if not args.no_e2e:
-        result["e2e_pcie"] = e2e_leg(drv, pristine if args.inplace else arena, desc, d, n, pkt_bytes,
+        result["e2e_pcie"] = e2e_leg(drv, arena, desc, d, n, pkt_bytes,
                                      args, world, dist)
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(pristine if args.inplace else arena, d, sids, keys, args,
+        result["cpu_baseline"] = cpu_baseline(arena, d, sids, keys, args,
                                               n, cfg)
         try:
-            result["cpu_openssl"] = cpu_openssl(pristine if args.inplace else arena, d, sids, keys, args,
+            result["cpu_openssl"] = cpu_openssl(arena, d, sids, keys, args,
                                                 n, cfg)
         except Exception as e:                   # informational only (needs tools/libossl_esp.so)
             log("cpu_openssl skipped: %s" % e)
@@ -307,15 +345,17 @@ def main():
 
 def launched_kernel(cfg, inplace):
     """Source name of the kernel the timed loop launches (the one the roofline
-    prices): gcm_kernel<MODE, 1024, S, STAGE> with MODE 0 = out-of-place
-    decrypt, 2 = in-place verify-first, S = 4 lanes per record (every bench
+    prices): gcm_kernel<MODE, 1024, S, STAGE> with MODE 3 = decrypt in place,
+    verify first, in one pass (a failed record's keystream XORed back over it;
+    MODE 2, the two-pass in-place decrypt, is built with GCM_INPLACE_ONEPASS=0
+    only), MODE 0 = out of place, S = 4 lanes per record (every bench
     config has >= 32K records: the small-batch S = 8 kernel is not launched),
     STAGE false (device-resident records);
     eta_kernel<3 (out of place) / 2 (in place), 768, -2> for CBC + HMAC-SHA1
     (verify pass, then the block-parallel decrypt of the verified records; -2 =
     the launch for SHA-1 / SHA2-256 sessions, esp_cbc.hip CK_NARROW)."""
     if cfg["alg"] == "gcm":
-        return "gcm_kernel<%d, 1024, 4, false>" % (2 if inplace else 0)
+        return "gcm_kernel<%d, 1024, 4, false>" % (3 if inplace else 0)
     return "eta_kernel<2, 768, -2>" if inplace else "eta_kernel<3, 768, -2>"   # verify-first two-pass
 
 
@@ -347,26 +387,32 @@ def profile_traffic(config, inplace, kernel, kern_ms):
     return out
 
 
-def inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, algo_bytes, world, dist, kernel):
-    """The verify-first in-place decrypt (d_out == d_arena: two passes, failed
-    records keep their ciphertext) on the same records, beside the headline.
-    Each launch needs fresh ciphertext, so a restore copy runs before every
-    launch; only the decrypt launches are timed (HIP events on the stream)."""
+def side_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, algo_bytes, world, dist, kernel,
+             inplace):
+    """The other decrypt mode on the same records, beside the headline: the
+    verify-first in-place decrypt (d_out == d_arena: failed records keep their
+    ciphertext; GCM in one pass that rolls a failed record back, ETA in two
+    passes; a restore copy before every launch, untimed) or the out-of-place
+    single pass.  Only the decrypt launches are timed (HIP events on the
+    stream), median of 5."""
     import torch
     from espgpu.batch import decrypt_batch
-    work = arena.clone()
+    work = arena.clone() if inplace else None
+    dst = None if inplace else torch.empty_like(arena)
     reps = 5
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps + 1)]
     with torch.cuda.stream(stream):
         for e0, e1 in evs:
-            work.copy_(arena)
+            if inplace:
+                work.copy_(arena)
             e0.record(stream)
-            decrypt_batch(drv, work, desc, n, status, out=None, grouped=grouped, stream=stream)
+            decrypt_batch(drv, work if inplace else arena, desc, n, status, out=dst, grouped=grouped,
+                          stream=stream)
             e1.record(stream)
     torch.cuda.synchronize()
     ok = int((status != 0).sum()) == 0
     ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs[1:])[reps // 2]
-    del work
+    del work, dst
     if world > 1:
         t = torch.tensor([ms], dtype=torch.float64, device=arena.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -376,7 +422,7 @@ def inplace_leg(drv, arena, desc, n, status, grouped, stream, pkt_bytes, algo_by
     return {"value": round(pkt_bytes / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "kernel_ms": round(ms, 4),
             "achieved_algorithmic_GBps": round(algo_bytes / (ms * 1e-3) / 1e9, 1),
             "status_ok": ok, "timing": "median of %d launches, HIP events around the decrypt only" % reps,
-            "kernel": kernel + " (verify-first, in place)"}
+            "kernel": kernel + (" (verify-first, in place)" if inplace else " (out of place, single pass)")}
 
 
 def packed_leg(drv, arena, desc, d, n, status, grouped, stream, pkt_bytes, algo_bytes, world, dist):
@@ -618,7 +664,7 @@ def cpu_openssl(arena, d, sids, keys, args, n, cfg):
         kw = dict(alg="gcm", ckeys=[k[:-4] for k in keys], salts=[k[-4:] for k in keys], mlen=16)
     else:
         kw = dict(alg="cbc_sha1", ckeys=[k[0] for k in keys], akeys=[k[1] for k in keys], mlen=12)
-    # out of place (the headline's mode), the sample REPS times over per run,
+    # out of place (so the sample stays ciphertext), REPS times over per run,
     # so a run lasts ~1 s and the cgroup quota's 100-ms periods average out
     REPS = 8
     out = np.empty_like(host)

@@ -83,10 +83,19 @@
 #ifndef GCM_RING
 #define GCM_RING 0
 #endif
+// In-place decrypt, verify first (fused kernel, S = 4 and 8): 1 = one pass that decrypts
+// in place while hashing and rolls a failed record back (CTR is its own
+// inverse: the same keystream XORed over the plaintext restores the
+// ciphertext bit for bit); 0 = MODE 2's two passes (GHASH + tag, then CTR
+// over the authenticated records only)
+#ifndef GCM_INPLACE_ONEPASS
+#define GCM_INPLACE_ONEPASS 1
+#endif
 
 namespace espgpu {
 
 namespace {
+constexpr int kGcmInPlaceMode = GCM_INPLACE_ONEPASS ? 3 : 2;   // do_group MODE of an in-place decrypt
 
 // LDS: the 8-bit H^S GHASH table at 0 (value-major, gf_mul8), the AES
 // T-table at 64 KiB.
@@ -570,6 +579,8 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
 // MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
+// MODE 3: decrypt in place, verify first, in one pass: MODE 0 over the record
+//         itself, then a failed record's keystream XORed over it again
 // Steps m, m+1 of a lane run together: 2 independent AES blocks, then
 // GHASH as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with the 8-bit table.
 template <int MODE, int S, bool RING = false>
@@ -742,7 +753,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         st_partial(orec + 16 + 16 * c, o, rem);
         return mask_block(o, rem);
       }
-      if (MODE == 0) {
+      if (MODE == 0 || MODE == 3) {
         const uint4 pt = xor4(C, ks);
         if (!(gopts() & 9)) st_partial(orec + 16 + 16 * c, pt, rem);
         note_trailer(i, pt, rem);
@@ -791,7 +802,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       const int rem = ct_len - 16 * j;
       const uint4 o = xor4(C, ks);
       if (!RING && !(gopts() & 9)) st_partial(orec + 16 + 16 * j, o, rem);
-      if (MODE == 0) note_trailer(j + 1, o, rem);
+      if (MODE == 0 || MODE == 3) note_trailer(j + 1, o, rem);
       return mask_block(MODE == 1 ? o : C, rem);
     };
     uint4 prev = (valid && l == S - 1) ? (sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0))
@@ -1000,6 +1011,29 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     } else {
       const uint4 d = mask_block(xor4(T, tag), (int)mlen);
       ok = ((d.x | d.y | d.z | d.w) == 0);
+    }
+  }
+  if (MODE == 3 && __any(valid && !ok)) {
+    // In place, one pass (MODE 3, GCM_INPLACE_ONEPASS): a record whose tag
+    // failed already holds plaintext; XORing the same keystream over it again
+    // restores the ciphertext exactly, so the buffer ends as cryptosoft's
+    // verify-first leaves it (cryptosoft.c:595-633: a failed record is not
+    // decrypted).  Rare path, one block per lane per step (small code): it
+    // runs only in a wave with a failed record, after the wave's stores are
+    // complete (the block-to-lane map here differs from the GHASH schedule's).
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const int back = valid && !ok;
+    int Mr = back ? (nct + S - 1) / S : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
+    for (int a = 0; a < Mr; ++a) {
+      const int c = S * a + l;
+      const uint32_t t = (uint32_t)c + 2;
+      uint4 P = make_uint4(0, 0, 0, 0);
+      if (back && c < nct) P = ld16(rec + 16 + 16 * c);
+      if ((int)(t >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(t >> 8), rk, lds, slot);
+      const uint4 ks = aes_ctr(cc, t, rk3, nr, rk, lds, slot);
+      if (back && c < nct) st_partial(rec + 16 + 16 * c, xor4(P, ks), ct_len - 16 * c);
     }
   }
   if (MODE == 2) {
@@ -2284,13 +2318,13 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
     if (encrypt)
       hipLaunchKernelGGL((gcm_kernel<1, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
     else if (two_pass)
-      hipLaunchKernelGGL((gcm_kernel<2, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
+      hipLaunchKernelGGL((gcm_kernel<kGcmInPlaceMode, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
     else
       hipLaunchKernelGGL((gcm_kernel<0, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
   } else if (encrypt) {
     hipLaunchKernelGGL((gcm_kernel<1, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
   } else if (two_pass) {
-    hipLaunchKernelGGL((gcm_kernel<2, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<kGcmInPlaceMode, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
   } else {
     hipLaunchKernelGGL((gcm_kernel<0, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
   }

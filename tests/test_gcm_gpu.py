@@ -225,6 +225,50 @@ def test_batch_inplace_verify_first(drv, gcm_lanes):
     drv.freesession(sids[0])
 
 
+@pytest.mark.parametrize("grouped", [True, False])
+@pytest.mark.parametrize("shape", ["aligned", "mixed"])
+def test_inplace_failed_records_restored_vs_oracle(drv, gcm_lanes, grouped, shape):
+    """In place, verify first, with forged records in every schedule the 4-lane
+    kernel has: it decrypts in one pass and XORs the keystream back over a
+    record whose tag failed (esp_gcm.hip GCM_INPLACE_ONEPASS), so the whole
+    arena must equal the oracle's in-place result byte for byte (a failed
+    record untouched, cryptosoft.c:595-633).  "aligned": 1448-byte payloads
+    only (the dense-AES schedule); "mixed": sizes that break it.  Forgeries in
+    the AAD, the ciphertext (first, middle and last block) and the ICV, one
+    whole wave of failed records, and single failures among good ones."""
+    from espgpu.batch import decrypt_batch
+    rng = np.random.default_rng(4106)
+    nsa = 1 if grouped else 12
+    sas = [GcmSA(rng, int(rng.choice([16, 32])), esn=bool(k % 2)) for k in range(nsa)]
+    sids = _sessions(drv, sas)
+    n = 2048
+    sa_idx = np.zeros(n, dtype=np.int64) if grouped else rng.integers(0, nsa, n)
+    cts = np.full(n, 1448) if shape == "aligned" else rng.choice([12, 204, 1448, 8948, 1452], n)
+    esn = rng.integers(0, 2**32, n, dtype=np.uint32)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, esn_hi=esn)
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    bad = ct.copy()
+    flip = rng.random(n) < 0.05
+    flip[64:80] = True                       # a whole wave (16 records of 4 lanes) fails
+    for k, i in enumerate(np.nonzero(flip)[0]):
+        o, L, alen = int(descs["off4"][i]) * 4, int(descs["len"][i]), sas[sa_idx[i]].mlen
+        ctl = L - 16 - alen
+        pos = [o + 5, o + 16, o + 16 + ctl // 2, o + 16 + ctl - 1, o + L - 1][k % 5]
+        bad[pos] ^= 1 << (k % 8)
+    ref, ref_st = oracle_decrypt(sas, bad, descs, eh)
+    assert (ref_st[flip] == O.EBADMSG).all() and (ref_st[~flip] == 0).all()
+    arena = _dev(bad)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    decrypt_batch(drv, arena, _descs_dev(d), n, st, out=None, grouped=grouped)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == ref_st).all()
+    res = arena.cpu().numpy()
+    assert (res == ref).all(), "first differing byte %d" % int(np.argmax(res != ref))
+    for s in sids:
+        drv.freesession(s)
+
+
 def test_planner_many_sessions_mixed_sizes(drv, gcm_lanes):
     """Random SA per record (the cfg2 shape, scaled down): device planner path."""
     from espgpu.batch import decrypt_batch

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run into profiles/<tag>.json (+ pmc_<cfg>.json).
 
-  python tools/prof_summary.py gpurun_out/prof_<tag> <tag> [cfg] [--inplace]
+  python tools/prof_summary.py gpurun_out/prof_<tag> <tag> [cfg] [--out-of-place]
 
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
@@ -79,8 +79,8 @@ def pipes(c, kern_ms):
 
 
 def main():
-    argv = [a for a in sys.argv[1:] if a != "--inplace"]
-    inplace = "--inplace" in sys.argv
+    argv = [a for a in sys.argv[1:] if a not in ("--inplace", "--out-of-place")]
+    inplace = "--out-of-place" not in sys.argv      # bench.py's headline is the in-place decrypt
     d, tag = argv[0], argv[1]
     cfg = argv[2] if len(argv) > 2 else "cfg1"
     ks = kernel_stats(d)

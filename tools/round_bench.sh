@@ -6,15 +6,15 @@
 set -e
 TAG=${1:?tag}
 mkdir -p gpurun_out/profiles
-prof() {   # <name> <cfg> [--inplace]
+prof() {   # <name> <cfg> [--out-of-place]
   bash tools/profile.sh ${TAG}_$1 --config $2 $3 > gpurun_out/prof_${TAG}_$1.log 2>&1
   python tools/prof_summary.py gpurun_out/prof_${TAG}_$1 ${TAG}_$1 $2 $3 > gpurun_out/sum_${TAG}_$1.log 2>&1
   echo "profile $1 done"
 }
 # PROFS / BENCHES select a subset (a call has at most 20 minutes)
-for p in ${PROFS-cfg1 cfg2 cfg3 cfg4 cfg0 cfg1_inplace}; do
+for p in ${PROFS-cfg1 cfg2 cfg3 cfg4 cfg0 cfg1_oop}; do
   case $p in
-    cfg1_inplace) prof cfg1_inplace cfg1 --inplace ;;
+    cfg1_oop) prof cfg1_oop cfg1 --out-of-place ;;
     *) prof $p $p ;;
   esac
 done
