@@ -231,7 +231,9 @@ int  espgpu_get_stats(espgpu_ctx *ctx, struct espgpu_stats *st);
  * d_arena: device buffer holding the records (padded by >= 16 bytes at its
  * end); d_desc[n]; d_status[n] receives one errno byte per record.
  * decrypt: plaintext goes to d_out at the same offsets (d_out may equal
- * d_arena: then a verify-first two-pass kernel keeps EBADMSG records intact).
+ * d_arena: verify-first in place; an EBADMSG record ends byte-identical to
+ * its ciphertext: AES-GCM in one pass that XORs the keystream back over a
+ * failed record, CBC/CTR + HMAC verifying before it decrypts).
  * encrypt: payload encrypted in place, ICV written.
  * `flags`: ESPGPU_BATCH_GROUPED if d_desc is already grouped by session with
  * at most one session per aligned run of 256 records (skips the device

@@ -12,8 +12,8 @@ case ${1:?part} in
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4_final_smoke.log 2>&1
     echo smoke done ;;
   prof)
-    BENCHES="" bash tools/round_bench.sh r4
-    for d in gpurun_out/prof_r4_*/; do d=${d%/}; cp $d/trace/run_kernel_stats.csv gpurun_out/profiles/$(basename $d | sed 's/^prof_//')_kernel_stats.csv; done ;;
+    BENCHES="" bash tools/round_bench.sh ${TAG:-r4}
+    for d in gpurun_out/prof_${TAG:-r4}_*/; do d=${d%/}; cp $d/trace/run_kernel_stats.csv gpurun_out/profiles/$(basename $d | sed 's/^prof_//')_kernel_stats.csv; done ;;
   bench)
-    PROFS="" bash tools/round_bench.sh r4 ;;
+    PROFS="" bash tools/round_bench.sh ${TAG:-r4} ;;
 esac
