@@ -91,6 +91,13 @@
 #ifndef GCM_INPLACE_ONEPASS
 #define GCM_INPLACE_ONEPASS 1
 #endif
+// Final multiply from LDS (planner batches, S = 4 kernel): lane 0's H^4 from
+// the resident 8-bit table, lanes 1-3's H^3..H^1 from 4-bit tables staged
+// value-major (24 KiB) with the session's GHASH table, instead of gathers of
+// the 32 KiB power tables from L2 (which miss once a batch has many sessions)
+#ifndef GCM_FMUL_LDS
+#define GCM_FMUL_LDS 0
+#endif
 
 namespace espgpu {
 
@@ -102,6 +109,8 @@ constexpr int kGcmInPlaceMode = GCM_INPLACE_ONEPASS ? 3 : 2;   // do_group MODE 
 constexpr uint32_t LDS_GT = 0;          // H^S, 256 values x 16 positions x 16 B
 constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
 constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
+constexpr uint32_t LDS_FM = LDS_BYTES;     // GCM_FMUL_LDS: H^1..H^3 4-bit tables, value-major
+constexpr uint32_t kFmBytes = 3 * kGhPowerBytes;
 // The output ring after them (gcm_kernel with RING): 128 bytes per record in
 // flight, 256 records per workgroup = the 32 KiB the tables leave of 160 KiB.
 constexpr uint32_t LDS_RING = LDS_BYTES;
@@ -532,6 +541,29 @@ __device__ __forceinline__ uint4 gf_mul8_wide(uint4 x, const uint8_t *lds, const
   return make_uint4(r0, r1, r2, r3);
 }
 
+// Y * H^e with a 4-bit table in LDS at `base`, value-major (value n, nibble
+// position j at n*512 + j*16: GCM_FMUL_LDS).  Lane L walks the positions of
+// each half in the order t ^ (L & 15), so the 16 lanes of a ds_read_b128 group
+// read 16 different bank quads whatever their values.
+__device__ __forceinline__ uint4 gf_mul4_lds(uint4 x, const uint8_t *lds, uint32_t base, int lane) {
+  const uint32_t lm = (uint32_t)lane & 15u;
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll 2
+  for (int t = 0; t < 16; ++t) {
+    const uint32_t q = (uint32_t)t ^ lm;
+    const uint32_t sh = (q & 7u) * 4u;
+    const uint32_t wl = (q & 8u) ? x.y : x.x, wh = (q & 8u) ? x.w : x.z;
+    const uint4 e = *reinterpret_cast<const uint4 *>(lds + base + ((wl >> sh) & 15u) * 512u + q * 16u);
+    const uint4 f = *reinterpret_cast<const uint4 *>(lds + base + ((wh >> sh) & 15u) * 512u + (16u + q) * 16u);
+    r0 = xor3(r0, e.x, f.x);
+    r1 = xor3(r1, e.y, f.y);
+    r2 = xor3(r2, e.z, f.z);
+    r3 = xor3(r3, e.w, f.w);
+    asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
+  }
+  return make_uint4(r0, r1, r2, r3);
+}
+
 // Y * H^e with the 4-bit table of that power in global memory (t = its 8 KiB:
 // nibble position j (byte j>>1, low nibble if j even), value n at j*256+n*16).
 // Used once per record per lane (the final x H^(8-l)), where the power differs
@@ -583,9 +615,10 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 //         itself, then a failed record's keystream XORed over it again
 // Steps m, m+1 of a lane run together: 2 independent AES blocks, then
 // GHASH as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with the 8-bit table.
-template <int MODE, int S, bool RING = false>
+template <int MODE, int S, bool RING = false, bool FM = false>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
-                                         uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk) {
+                                         uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk,
+                                         bool fm = false) {
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
   const uint32_t slot = ((uint32_t)(lane & 31) * 4) | (LDS_TP & 0xff0000u);
@@ -996,8 +1029,13 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     }
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
-  uint4 Z = (gopts() & 64) ? Y
-                           : gf_mul4_global<true>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+  uint4 Z;
+  if (gopts() & 64)
+    Z = Y;
+  else if (FM && fm)
+    Z = l == 0 ? gf_mul8(Y, lds, gl) : gf_mul4_lds(Y, lds, LDS_FM + (uint32_t)(S - 1 - l) * kGhPowerBytes, lane);
+  else
+    Z = gf_mul4_global<true>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 ej0 = shfl4(EJ0, (lane & ~(S - 1)) | pad);
@@ -1483,7 +1521,8 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
   // the output ring (do_group): the headline decrypt's shape only
   constexpr bool RING = GCM_RING && MODE == 0 && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0)];
+  constexpr bool FM = GCM_FMUL_LDS && !RING && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0) + (FM ? kFmBytes : 0)];
   const int tid = threadIdx.x;
   GCM_PHASE(0, true);
   // The T-table (per entry 32 slots of Te0 then 32 slots of Te1, see tpa())
@@ -1551,6 +1590,15 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
           uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
 #pragma unroll 4
           for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+          if (FM && !implicit) {
+            // H^1..H^3 (power index i = 0..2): position-major in gtab (j*256 +
+            // n*16), value-major here (n*512 + j*16)
+            const uint4 *pw = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes);
+            for (int q = tid; q < (int)(kFmBytes / 16); q += WG) {
+              const int i = q >> 9, j = (q >> 4) & 31, nv = q & 15;
+              *reinterpret_cast<uint4 *>(lds + LDS_FM + i * kGhPowerBytes + nv * 512 + j * 16) = pw[q];
+            }
+          }
         }
       } else {
         mode = 0;
@@ -1581,7 +1629,8 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         continue;
       }
-      do_group<MODE, S, RING>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
+      do_group<MODE, S, RING, FM>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk),
+                                  !implicit);
     }
     GCM_PHASE(5, it == 0);
     if (STAGE) {
