@@ -221,6 +221,10 @@ def main():
     if inplace:
         free = torch.cuda.mem_get_info(dev)[0]
         ncopy = max(1, min(args.steps, int(free * 0.6) // total))
+        if world > 1:            # the same segments on every rank (their barriers pair up)
+            t = torch.tensor([ncopy], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ncopy = int(t.item())
         bufs = [arena.clone() for _ in range(ncopy)]
     else:
         bufs = [arena]
