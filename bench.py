@@ -155,11 +155,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a one-GPU box (never a measurement):
+    # BENCH_SHARE_DEVICE=1 puts every rank on device 0 and BENCH_DIST_BACKEND=gloo
+    # replaces RCCL, which refuses two ranks on one device
+    if os.environ.get("BENCH_SHARE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
