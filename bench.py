@@ -58,6 +58,17 @@ def aggregate(dist, world, dt, nbytes, device):
     return float(t.item()), int(b.item())
 
 
+def agree_min(dist, world, value, device):
+    """The smallest of the ranks' values (every rank gets it): the in-place
+    copy count, so all ranks run the same timed segments."""
+    if world == 1:
+        return value
+    import torch
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
 def per_rank(dist, world, rank, value, device):
     """[value of rank 0, ..., value of rank world-1] (one all_reduce)."""
     if world == 1:
@@ -230,10 +241,7 @@ def main():
     if inplace:
         free = torch.cuda.mem_get_info(dev)[0]
         ncopy = max(1, min(args.steps, int(free * 0.6) // total))
-        if world > 1:            # the same segments on every rank (their barriers pair up)
-            t = torch.tensor([ncopy], dtype=torch.int64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            ncopy = int(t.item())
+        ncopy = agree_min(dist, world, ncopy, dev)   # the same segments on every rank
         bufs = [arena.clone() for _ in range(ncopy)]
     else:
         bufs = [arena]

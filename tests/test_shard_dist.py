@@ -82,6 +82,8 @@ def _rank_main(rank, world, port, q):
         dist.all_gather_object(got, (sorted(spis), len(sizes)))
         counts = bench.per_rank(dist, world, rank, len(sizes), torch.device("cpu"))
         assert counts == [g[1] for g in got]
+        # in-place copies: every rank takes the smallest count (equal segments)
+        assert bench.agree_min(dist, world, 20 - 7 * rank, torch.device("cpu")) == 13
         q.put((rank, mdt, total, nbytes, got))
     finally:
         dist.destroy_process_group()
