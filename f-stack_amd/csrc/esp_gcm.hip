@@ -40,6 +40,10 @@
 //  * Records are read and written with single 16-byte vector accesses, 128
 //    contiguous bytes per record per paired step.  HBM traffic per record =
 //    record + descriptor + plaintext + status byte.
+//  * In place (d_out == d_arena, the opencrypto contract) the same single
+//    pass decrypts over the ciphertext it hashes (MODE 3); a record whose tag
+//    fails gets the same keystream XORed over it once more, which restores its
+//    ciphertext exactly (cryptosoft.c:595-633 never decrypts such a record).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
