@@ -762,6 +762,9 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = bswap32(m[k]);
     } else if (on && b < total) {
+      // the hash words first: in place, the stores below overwrite the tail
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
       if (b == nfull) {
         // the cipher blocks after the last full chunk (1..4 of them)
         if (CK == CK_CBC) {
@@ -809,8 +812,6 @@ __device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *o
           }
         }
       }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
     } else {
       outer_block<HS>(h, w);
       if (on) {
@@ -1451,6 +1452,13 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     // kernel per cipher plus MODE 3 for SHA2-384/512 (eta_fused = 1)
     // (kinds bit 4: HMAC-SHA2-384/512 sessions exist, served by their own launch)
     if (in_place) {
+#if defined(ESPGPU_VARIANTS) && defined(ETA_INPLACE_PROBE)
+      // timing probe only (no rollback of failed records): the one-pass MODE 0
+      // over the records in place
+      if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+#endif
       hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
 #ifdef ESPGPU_VARIANTS
