@@ -142,13 +142,26 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return perm(x, x, 0x00
 // operations (one IR access each, so the backend never splits or re-merges them)
 typedef uint32_t V4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t V2a __attribute__((ext_vector_type(2), aligned(4)));
+// GCM_NT (measurement switch): bit 0 = nontemporal record loads, bit 1 =
+// nontemporal stores (the streaming hint on the vector memory instructions)
+#ifndef GCM_NT
+#define GCM_NT 0
+#endif
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+#if GCM_NT & 1
+  const V4a v = __builtin_nontemporal_load(reinterpret_cast<const V4a *>(p));
+#else
   const V4a v = *reinterpret_cast<const V4a *>(p);
+#endif
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
   V4a u = {v.x, v.y, v.z, v.w};
+#if GCM_NT & 2
+  __builtin_nontemporal_store(u, reinterpret_cast<V4a *>(p));
+#else
   *reinterpret_cast<V4a *>(p) = u;
+#endif
 }
 __device__ __forceinline__ void st8(uint8_t *p, uint32_t a, uint32_t b) {
   V2a u = {a, b};
