@@ -26,7 +26,10 @@ namespace espgpu {
 namespace {
 
 constexpr int PWG = 1024;
-constexpr int PER_THREAD = 4;
+#ifndef PLAN_PER_THREAD
+#define PLAN_PER_THREAD 4
+#endif
+constexpr int PER_THREAD = PLAN_PER_THREAD;   // records per thread of count / scatter
 constexpr int TILE = PWG * PER_THREAD;
 constexpr uint32_t kMaxLdsKeys = 16384;   // 64 KiB per LDS array
 
