@@ -7,7 +7,7 @@ mkdir -p gpurun_out/r4_pt
 ESPGPU_LIB=abl/pt16/libespgpu.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
   tests/test_configs_gpu.py tests/test_eta_gpu.py > gpurun_out/r4_pt/tests.log 2>&1
 tail -1 gpurun_out/r4_pt/tests.log
-for CFG in cfg4 cfg2 cfg3; do
+for CFG in ${CFGS:-cfg4 cfg2}; do
   for k in 1 2 3; do
     for L in f-stack_amd/libespgpu.so abl/pt8/libespgpu.so abl/pt16/libespgpu.so; do
       echo -n "$CFG $L "
