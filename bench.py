@@ -129,6 +129,90 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` without a torch.distributed launcher around us: start N ranks
+    as ONE child process (`python -m torch.distributed.run --nproc-per-node N
+    bench.py ...`, rendezvous on 127.0.0.1), relay rank 0's JSON line after
+    checking it reports N GPUs, and return the child's exit code.  Called
+    before anything touches the GPU (torch.cuda.device_count() does not
+    initialise HIP on this image); the parent never execs."""
+    import subprocess
+    n = args.gpus
+    if not args.dry_plan and os.environ.get("BENCH_SHARE_DEVICE") != "1":
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            log("bench.py: --gpus %d but this node has %d GPU(s); refusing to report a smaller run" % (n, have))
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + argv
+    log("bench.py: launching %d ranks: %s" % (n, " ".join(cmd)))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for raw in proc.stdout:                 # ranks' stdout; only rank 0 prints the JSON line
+        s = raw.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        else:
+            sys.stderr.write(raw)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        log("bench.py: the %d-rank run exited with %d" % (n, rc))
+        return rc
+    if line is None:
+        log("bench.py: the %d-rank run printed no result line" % n)
+        return 4
+    res = json.loads(line)
+    if res.get("n_gpus") != n or res.get("config", {}).get("world") != n:
+        log("bench.py: asked for %d GPUs, the run reports n_gpus=%s world=%s"
+            % (n, res.get("n_gpus"), res.get("config", {}).get("world")))
+        return 5
+    print(line, flush=True)
+    return 0
+
+
+def dry_plan(args, world, rank, local):
+    """--dry-plan: the rank logic of a run without a GPU (gloo, CPU tensors):
+    each rank plans its share of the config's packets (SPI-hash sharding) and
+    rank 0 prints the JSON line's shape with world, packets_per_rank and the
+    device ids, so the N-rank launch path is testable on a CPU host."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = dict(CONFIGS[args.config])
+    if args.packets:
+        cfg["packets"] = args.packets
+    rng = np.random.default_rng(0xE5B00001 + rank)
+    spis, sa_of, sizes = plan_packets(cfg, rank, world, rng)
+    cpu = torch.device("cpu")
+    n = len(sizes)
+    res = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": 0,
+           "warmup": 0, "dry_plan": True,
+           "config": {"workload": cfg["workload"], "world": world,
+                      "packets_per_rank": per_rank(dist, world, rank, n, cpu),
+                      "sas_per_rank": per_rank(dist, world, rank, len(spis), cpu),
+                      "device_per_rank": per_rank(dist, world, rank, local, cpu)}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+METRIC = "GB/s device-resident ESP AES-128-GCM decrypt, 1M×1500B pkts, 1/2/4/8 GPU"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,15 +241,30 @@ def main():
     ap.add_argument("--e2e-chunk", type=int, default=65536, help="records per pipelined step")
     ap.add_argument("--out-pad", type=int, default=0,
                     help="experiment: extra bytes per record in the out-of-place buffer (layout probes)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-plan", action="store_true",
+                    help="test aid: run the N-rank launch and each rank's packet plan on gloo/CPU, no GPU")
+    ap.add_argument("--packets", type=int, default=0, help="with --dry-plan: packets per GPU override")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
     inplace = not args.out_of_place
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_plan:
+        dry_plan(args, world, rank, local)
+        return
 
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N-rank path on a one-GPU box (never a measurement):
     # BENCH_SHARE_DEVICE=1 puts every rank on device 0 and BENCH_DIST_BACKEND=gloo
     # replaces RCCL, which refuses two ranks on one device
@@ -301,8 +400,9 @@ def main():
     kern_ms = ev_ms / args.steps
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
 
+    assert world == args.gpus, "n_gpus %d != --gpus %d" % (world, args.gpus)
     result = {
-        "metric": "GB/s device-resident ESP AES-128-GCM decrypt, 1M×1500B pkts, 1/2/4/8 GPU",
+        "metric": METRIC,
         "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
@@ -327,8 +427,11 @@ def main():
         result["roofline"]["frac_of_copy"] = round(achieved / copy, 4)
     except Exception as e:                       # informational only
         log("hbm copy measurement skipped: %s" % e)
+    result["config"]["world"] = world
+    result["config"]["packets_per_rank"] = per_rank(dist, world, rank, n, dev)
+    result["config"]["device_per_rank"] = per_rank(dist, world, rank, local, dev)
     if world > 1:
-        result["config"]["packets_per_rank"] = per_rank(dist, world, rank, n, dev)
+        result["config"]["distinct_devices"] = len(set(result["config"]["device_per_rank"]))
     if inplace:
         result["config"]["inplace_copies"] = ncopy
     kernel = launched_kernel(cfg, inplace)

@@ -1896,12 +1896,18 @@ __global__ __launch_bounds__(WG) void gcm_door_kernel(DoorArgs a) {
   for (uint32_t it = 0;; ++it) {
     uint32_t *cmd = s_cmd[it & 1];
     if (tid == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint32_t job = kExit, c = 0, n = 0, so = 0;
+      uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t job = kExit, c = 0, n = 0, so = 0, stop = 0;
       typedef uint32_t V4 __attribute__((ext_vector_type(4)));
       for (uint32_t poll = 0;; ++poll) {
-        // (stop is read on every 4th poll: each read is a PCIe round trip)
-        if ((poll & 3) == 0 && *reinterpret_cast<volatile uint32_t *>(&a.ctl->stop)) break;
+        // stop (read on every 4th poll: each read is a PCIe round trip):
+        // kDoorStopNow exits between chunks; kDoorStopIdle (the host is about
+        // to launch other kernels, which may share this kernel's hardware
+        // queue) exits as soon as no published job is waiting
+        if ((poll & 3) == 0) {
+          stop = *reinterpret_cast<volatile uint32_t *>(&a.ctl->stop);
+          if (stop == kDoorStopNow) break;
+        }
         if (!have) {
           const uint32_t hint = __hip_atomic_load(&a.dev->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((int32_t)(hint - cur) > 0) cur = hint;
@@ -1909,10 +1915,14 @@ __global__ __launch_bounds__(WG) void gcm_door_kernel(DoorArgs a) {
           if (e.w == cur + 1 && e.z == (e.x ^ e.y ^ e.w ^ kDoorChk)) {
             have = true;
             en = e.x, eso = e.y, enc = (e.x + a.chunk - 1) / a.chunk;
+            // jobs are still arriving: the idle clock restarts even if other
+            // workgroups win every chunk of this one
+            t0 = __builtin_amdgcn_s_memrealtime();
           } else if ((int32_t)(e.w - (cur + 1)) > 0) {
             ++cur;                         // the entry holds a later job: job cur is long done
             continue;
           } else {
+            if (stop == kDoorStopIdle) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.idle_ticks) break;
             __builtin_amdgcn_s_sleep(4);
             continue;

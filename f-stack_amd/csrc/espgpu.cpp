@@ -17,6 +17,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -74,31 +75,77 @@ struct OvfEntry {
   int32_t sid;
   uint8_t op, kind;
 };
-struct Overflow {
-  std::vector<OvfEntry> ent;
-  size_t head = 0;            // first entry not yet moved into a slot
-  std::vector<uint8_t> bytes;
-  std::vector<espgpu_seg> segpool;
-  bool empty() const { return head == ent.size(); }
-  // live bytes only: entries already moved into slots no longer count
-  size_t footprint() const {
-    return empty() ? 0 : bytes.size() - ent[head].pd.stage_off + (ent.size() - head) * sizeof(OvfEntry);
+// A fixed-capacity FIFO of variable-length contiguous allocations (a bip
+// buffer): allocated in arrival order, freed oldest first, wrapping to the
+// start when the end has no room.  Allocated once; never grows or moves, so
+// process() never reallocates or copies it.
+template <class T>
+struct FifoArena {
+  std::unique_ptr<T[]> buf;
+  size_t cap = 0, head = 0, tail = 0;
+  bool wrapped = false;              // the newest allocations sit in [0, tail) below head
+  void init(size_t n) {
+    buf.reset(n ? new T[n] : nullptr);
+    cap = n;
+    clear();
   }
-  void reset() { ent.clear(); head = 0; bytes.clear(); segpool.clear(); }
-  // drop the moved prefix (flush, once it is at least half the entries) so a
-  // sustained load that never empties the overflow does not grow it
-  void compact() {
-    if (empty()) { reset(); return; }
-    if (head < 64 || 2 * head < ent.size()) return;
-    const uint32_t b0 = ent[head].pd.stage_off, s0 = ent[head].pd.seg0;
-    bytes.erase(bytes.begin(), bytes.begin() + b0);
-    segpool.erase(segpool.begin(), segpool.begin() + s0);
-    ent.erase(ent.begin(), ent.begin() + (ptrdiff_t)head);
-    for (OvfEntry &e : ent) {
-      e.pd.stage_off -= b0;
-      e.pd.seg0 -= s0;
+  void clear() { head = tail = 0; wrapped = false; }
+  struct Mark { size_t head, tail; bool wrapped; };
+  Mark mark() const { return {head, tail, wrapped}; }
+  void undo(const Mark &m) { head = m.head; tail = m.tail; wrapped = m.wrapped; }
+  // offset of n contiguous elements, or SIZE_MAX when there is no room
+  size_t alloc(size_t n) {
+    if (n == 0) return 0;
+    if (!wrapped) {
+      if (tail + n <= cap) { tail += n; return tail - n; }
+      if (n <= head) { wrapped = true; tail = n; return 0; }
+      return SIZE_MAX;
     }
-    head = 0;
+    if (tail + n <= head) { tail += n; return tail - n; }
+    return SIZE_MAX;
+  }
+  // free the oldest allocation [off, off + n)
+  void pop(size_t off, size_t n) {
+    if (n == 0) return;
+    if (wrapped && off < head) wrapped = false;    // the first allocation after the wrap
+    head = off + n;
+  }
+};
+
+// The host overflow: entries in a fixed ring, their gathered bytes and segment
+// lists in fixed FIFO arenas, all sized at set_tuning("overflow_mb").
+struct Overflow {
+  std::unique_ptr<OvfEntry[]> ent;
+  size_t ecap = 0, head = 0, count = 0;   // ring of entries; head = oldest
+  FifoArena<uint8_t> bytes;
+  FifoArena<espgpu_seg> segpool;
+  size_t live_bytes = 0, peak_bytes = 0;
+  bool empty() const { return count == 0; }
+  OvfEntry &front() { return ent[head]; }
+  void init(size_t cap_bytes) {
+    // the byte ring holds overflow_mb of records; entries (a zero-copy record
+    // needs no bytes) and segment lists get rings of their own beside it
+    ecap = cap_bytes ? std::max<size_t>(256, std::min<size_t>(cap_bytes / 512, (size_t)1 << 22)) : 0;
+    ent.reset(ecap ? new OvfEntry[ecap] : nullptr);
+    bytes.init(cap_bytes);
+    segpool.init(ecap * 4);
+    head = count = 0;
+    live_bytes = peak_bytes = 0;
+  }
+  size_t reserved() const {
+    return ecap * sizeof(OvfEntry) + bytes.cap + segpool.cap * sizeof(espgpu_seg);
+  }
+  void pop() {
+    OvfEntry &e = ent[head];
+    if (!e.pd.zc) bytes.pop(e.pd.stage_off, (e.pd.stage_len + 15) & ~15u);
+    segpool.pop(e.pd.seg0, e.pd.nsegs);
+    live_bytes -= e.pd.zc ? 0 : ((e.pd.stage_len + 15) & ~15u);
+    head = (head + 1) % ecap;
+    if (--count == 0) {
+      head = 0;
+      bytes.clear();
+      segpool.clear();
+    }
   }
 };
 
@@ -215,6 +262,7 @@ struct espgpu_ctx {
   // batches of <= gcm_burst records with no launch per batch
   int door_wg = 0;
   uint32_t door_idle_us = 20000;             // the kernel exits after this long without a job
+  bool door_retiring = false;                // kDoorStopIdle requested (door_retire)
   DoorCtl *door_ctl = nullptr, *door_ctl_dev = nullptr;
   DoorDev *d_door = nullptr;
   DoorSlot *d_door_slots = nullptr;
@@ -435,10 +483,25 @@ bool door_exited(espgpu_ctx *c) {
 // claim stay in the ring for the next launch).
 void door_stop(espgpu_ctx *c) {
   if (!c->door_live) return;
-  __atomic_store_n(&c->door_ctl->stop, 1u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&c->door_ctl->stop, kDoorStopNow, __ATOMIC_SEQ_CST);
   hipEventSynchronize(c->ev_door);
   __atomic_store_n(&c->door_ctl->stop, 0u, __ATOMIC_SEQ_CST);
   c->door_live = false;
+  c->door_retiring = false;
+}
+
+// Before any other kernel or copy of this ctx is queued: the persistent
+// kernel's stream may share a hardware queue with the stream that work goes
+// to (GPU_MAX_HW_QUEUES is 4; a ctx has more streams), and a queue runs its
+// packets in order, so work behind a resident door kernel would wait for its
+// idle timeout.  Without waiting, ask it to exit once no published job is
+// left (kDoorStopIdle): queued work starts right after its last chunk.  The
+// next door job clears the request and relaunches the kernel if it exited.
+void door_retire(espgpu_ctx *c) {
+  if (!c->door_live || c->door_retiring) return;
+  if (door_exited(c)) return;
+  __atomic_store_n(&c->door_ctl->stop, kDoorStopIdle, __ATOMIC_SEQ_CST);
+  c->door_retiring = true;
 }
 
 int door_launch(espgpu_ctx *c) {
@@ -453,6 +516,8 @@ int door_launch(espgpu_ctx *c) {
   a.gtab = c->d_gtab;
   a.tpair = c->d_tpair;
   a.nsas = c->cfg.max_sessions;              // unused entries are zero (mode 0): EINVAL
+  __atomic_store_n(&c->door_ctl->stop, 0u, __ATOMIC_SEQ_CST);
+  c->door_retiring = false;
   if (launch_gcm_door(a, c->door_wg, c->s_door)) return fail(c, ESPGPU_EIO, "door kernel launch failed");
   HIPCHK(c, hipEventRecord(c->ev_door, c->s_door));
   c->door_live = true;
@@ -548,6 +613,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   if (n == 0) return 0;
   if (out_stride && c->n_eta > 0)
     return fail(c, ESPGPU_ENOTSUP, "packed output serves contexts with GCM sessions only");
+  door_retire(c);
   if (c->launched && st != c->last_st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
   const uint32_t nsas = (uint32_t)c->sessions.size();
   GcmParams p{};
@@ -922,14 +988,16 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   // (doorbell jobs have no stream to wait on: drain them)
   if (c->ovf.empty() && !c->door_ctl) espgpu_flush(c);
   else espgpu_drain(c);
+  // the doorbell kernel keeps its current session's state (H^8 table in LDS);
+  // stopped before the stream syncs, which could otherwise wait behind it
+  // on a shared hardware queue
+  door_stop(c);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->s_out);
   for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
   // and the ctx's last launch on any stream: a device-resident batch on the
   // caller's stream may still be reading this slot's keys
   if (c->launched) hipEventSynchronize(c->ev_last);
-  // the doorbell kernel keeps its current session's state (H^8 table in LDS)
-  door_stop(c);
   const Session &fs = c->sessions[sid];
   if (fs.mode != ESPGPU_CSP_MODE_AEAD) {
     c->n_eta--;
@@ -1082,21 +1150,34 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
     }
   }
   if (to_ovf) {
+    // fixed rings reserved at set_tuning: nothing here allocates or moves
+    const uint64_t t_in = now_ns();
     Overflow &o = c->ovf;
-    const size_t add = (zc ? 0 : ((rlen + 15) & ~15u)) + sizeof(OvfEntry);
-    if (o.footprint() + add > c->ovf_cap) { c->stats.erestart++; return ESPGPU_ERESTART; }
-    pd.stage_off = (uint32_t)o.bytes.size();
-    if (!zc) {
-      o.bytes.resize(o.bytes.size() + ((rlen + 15) & ~15u));
-      if (!gather(o.bytes.data() + pd.stage_off)) {
-        o.bytes.resize(pd.stage_off);
-        return reject(ESPGPU_EINVAL);
-      }
+    const size_t blen = zc ? 0 : ((rlen + 15) & ~15u);
+    if (o.count == o.ecap) { c->stats.erestart++; return ESPGPU_ERESTART; }
+    const auto bm = o.bytes.mark();
+    const auto sm = o.segpool.mark();
+    const size_t boff = o.bytes.alloc(blen), soff = o.segpool.alloc((size_t)r->nsegs);
+    if (boff == SIZE_MAX || soff == SIZE_MAX) {
+      o.bytes.undo(bm);
+      o.segpool.undo(sm);
+      c->stats.erestart++;
+      return ESPGPU_ERESTART;
     }
-    pd.seg0 = (uint32_t)o.segpool.size();
-    o.segpool.insert(o.segpool.end(), r->segs, r->segs + r->nsegs);
-    o.ent.push_back(OvfEntry{pd, d, sid, (uint8_t)op, kind});
+    pd.stage_off = (uint32_t)boff;
+    if (!zc && !gather(o.bytes.buf.get() + boff)) {
+      o.bytes.undo(bm);
+      o.segpool.undo(sm);
+      return reject(ESPGPU_EINVAL);
+    }
+    pd.seg0 = (uint32_t)soff;
+    if (r->nsegs) memcpy(o.segpool.buf.get() + soff, r->segs, (size_t)r->nsegs * sizeof(espgpu_seg));
+    o.ent[(o.head + o.count) % o.ecap] = OvfEntry{pd, d, sid, (uint8_t)op, kind};
+    o.count++;
+    o.live_bytes += blen;
+    o.peak_bytes = std::max(o.peak_bytes, o.live_bytes);
     c->stats.overflow++;
+    c->stats.ovf_process_ns_max = std::max(c->stats.ovf_process_ns_max, now_ns() - t_in);
     return 0;
   }
   if (!zc && !gather(s->h_arena + s->bytes)) return reject(ESPGPU_EINVAL);
@@ -1161,6 +1242,21 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
         }
       }
     }
+    // a kernel asked to retire (launched work went by) may still be running:
+    // cancel the request before the job is visible, then relaunch if it (or
+    // an idle timeout since the last job) ended it.  Done before the ring
+    // entry is written, so a failed relaunch leaves nothing published.
+    const uint64_t t_pub = now_ns();
+    const bool was_retiring = c->door_retiring;
+    if (was_retiring) {
+      __atomic_store_n(&c->door_ctl->stop, 0u, __ATOMIC_SEQ_CST);
+      c->door_retiring = false;
+    }
+    if (!c->door_live || t_pub - c->door_last_pub > (uint64_t)c->door_idle_us * 500u ||
+        (was_retiring && door_exited(c))) {
+      e = door_ensure(c);
+      if (e) return e;
+    }
     const uint32_t j = c->door_next++;
     DoorJob &jb = c->door_ctl->ring[j % kDoorRing];
     const uint32_t so = (uint32_t)(&s - c->slots.data()) | ((uint32_t)s.op << 16);
@@ -1169,13 +1265,8 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
     jb.chk = s.nrec ^ so ^ (j + 1) ^ kDoorChk;
     __atomic_store_n(&jb.seq, j + 1, __ATOMIC_RELEASE);
     s.door_job = j;
-    s.door_t0 = now_ns();
-    // the kernel may have reached its idle timeout since the last job
-    if (!c->door_live || s.door_t0 - c->door_last_pub > (uint64_t)c->door_idle_us * 500u) {
-      e = door_ensure(c);
-      if (e) return e;
-    }
-    c->door_last_pub = s.door_t0;
+    s.door_t0 = t_pub;
+    c->door_last_pub = t_pub;
     s.timed = false;
     s.state = SLOT_INFLIGHT;
     c->stats.batches++;
@@ -1184,6 +1275,7 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
     c->cur = (c->cur + 1) % (int)c->slots.size();
     return 0;
   }
+  door_retire(c);                                  // launched work from here on
   if (small && c->stage_fused && one_gcm) {
     int e = xfer_reserve(c, s, 3 * s.nrec);
     if (e) return e;
@@ -1309,14 +1401,13 @@ int espgpu_flush(espgpu_ctx *c) {
     }
     if (o.empty() || s.state != SLOT_FREE) break;
     while (!o.empty()) {
-      const OvfEntry &en = o.ent[o.head];
+      const OvfEntry &en = o.front();
       if (slot_full(c, s, en.op, en.pd.stage_len)) break;
-      if (!en.pd.zc) memcpy(s.h_arena + s.bytes, o.bytes.data() + en.pd.stage_off, en.pd.stage_len);
-      slot_commit(s, en.pd, en.d, o.segpool.data() + en.pd.seg0, en.sid, en.op, en.kind);
-      o.head++;
+      if (!en.pd.zc) memcpy(s.h_arena + s.bytes, o.bytes.buf.get() + en.pd.stage_off, en.pd.stage_len);
+      slot_commit(s, en.pd, en.d, o.segpool.buf.get() + en.pd.seg0, en.sid, en.op, en.kind);
+      o.pop();
     }
   }
-  if (!o.ent.empty()) o.compact();
   return 0;
 }
 
@@ -1362,8 +1453,10 @@ int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
     if (s.state != SLOT_INFLIGHT) continue;
     if (s.door_job >= 0) {
       if (!door_done(c, s.door_job)) {
-        // outstanding for over 1 ms: make sure the kernel is still there
-        door_wait = now - s.door_t0 > 1000000u;
+        // outstanding for over 100 us: make sure the kernel is still there
+        // (a workgroup that read a retire request just before the job was
+        // published may have exited with it)
+        door_wait = now - s.door_t0 > 100000u;
         break;
       }
       s.door_job = -1;
@@ -1529,6 +1622,8 @@ int espgpu_replay_update(espgpu_replay *r, uint32_t *bitmap, uint32_t seq) {
 int espgpu_get_stats(espgpu_ctx *c, espgpu_stats *st) {
   if (!c || !st) return ESPGPU_EINVAL;
   *st = c->stats;
+  st->ovf_reserved = c->ovf.reserved();
+  st->ovf_peak = c->ovf.peak_bytes;
   return 0;
 }
 
@@ -1648,13 +1743,15 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!strcmp(key, "overflow_mb")) {
     // offsets into the overflow's byte buffer are 32-bit (Pending::stage_off)
     if (value < 0 || value > 4095) return ESPGPU_EINVAL;
+    // the rings are reserved whole here: growing the overflow inside
+    // process() would copy it (hundreds of microseconds at a few MiB).
+    // Resizing drains what the old rings hold first.
+    if (!c->ovf.empty()) {
+      int e = espgpu_drain(c);
+      if (e) return e;
+    }
     c->ovf_cap = (size_t)value << 20;
-    // reserved up front: growing the overflow inside process() would copy it
-    // (hundreds of microseconds at a few MiB)
-    const size_t rb = std::min(c->ovf_cap, (size_t)64 << 20), re = std::min(c->ovf_cap / 256, (size_t)1 << 18);
-    c->ovf.bytes.reserve(rb);
-    c->ovf.ent.reserve(re);
-    c->ovf.segpool.reserve(re);
+    c->ovf.init(c->ovf_cap);
     return 0;
   }
   if (!strcmp(key, "gcm_burst")) {

@@ -172,9 +172,11 @@ struct DoorJob {                                 // host-written; seq last (= jo
   uint32_t seq;
 };
 constexpr uint32_t kDoorChk = 0x5eed1e55u;
+constexpr uint32_t kDoorStopNow = 1;             // DoorCtl::stop: exit between chunks
+constexpr uint32_t kDoorStopIdle = 2;            // exit once no published job is waiting
 struct DoorCtl {                                 // pinned host memory, device-mapped
   DoorJob ring[kDoorRing];
-  uint32_t stop;
+  uint32_t stop;                                 // 0, kDoorStopNow or kDoorStopIdle
   uint32_t pad_[31];
   uint32_t done[kDoorRing];                      // job number + 1 once the job completed
 };

@@ -93,7 +93,8 @@ class Stats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("bytes", C.c_uint64), ("auth_fail", C.c_uint64),
                 ("einval", C.c_uint64), ("batches", C.c_uint64), ("kernel_ns", C.c_uint64),
                 ("erestart", C.c_uint64), ("overflow", C.c_uint64), ("zerocopy", C.c_uint64),
-                ("door", C.c_uint64)]
+                ("door", C.c_uint64), ("ovf_reserved", C.c_uint64), ("ovf_peak", C.c_uint64),
+                ("ovf_process_ns_max", C.c_uint64)]
 
 
 _lib = None

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define ESPGPU_ABI_VERSION 3
+#define ESPGPU_ABI_VERSION 4
 
 /* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
 #define ESPGPU_CSP_MODE_CIPHER      2        /* cryptodev.h:362: ESP without auth */
@@ -161,6 +161,10 @@ struct espgpu_stats {
 	uint64_t overflow;             /* requests staged through the host overflow      */
 	uint64_t zerocopy;             /* records moved from / to registered memory      */
 	uint64_t door;                 /* batches served by the doorbell kernel (ABI 3)  */
+	uint64_t ovf_reserved;         /* host bytes the overflow's fixed rings hold (ABI 4):
+	                                  set once by set_tuning "overflow_mb", never grown */
+	uint64_t ovf_peak;             /* most record bytes the overflow held at once    */
+	uint64_t ovf_process_ns_max;   /* longest overflow placement inside process()    */
 };
 
 typedef struct espgpu_ctx espgpu_ctx;

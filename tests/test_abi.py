@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     assert len(syms) >= 15
     for s in syms:
         assert hasattr(lib, s), "missing export %s" % s
-    assert lib.espgpu_abi_version() == 3
+    assert lib.espgpu_abi_version() == 4
 
 
 def test_struct_layouts():

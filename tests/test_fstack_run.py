@@ -219,6 +219,8 @@ def test_fstack_opencrypto_with_gpucrypto_gpu(workload, tmp_path):
     real host shim and libespgpu.so on the MI355X, against cryptosoft run in
     the same process, the DPDK known answers and the oracle."""
     exe = FR.EXE_GPU
-    if not os.path.exists(exe):
-        pytest.skip("integration/fstack_crypto_run_gpu is built where the F-Stack tree exists")
+    # built where the F-Stack tree exists (__graft_entry__.build) and shipped
+    # with the tree: a GPU run without it has lost the only F-Stack-level GPU
+    # check, which must show as a failure, not a skip
+    assert os.path.exists(exe), "integration/fstack_crypto_run_gpu missing: run __graft_entry__.build() where /root/reference exists"
     _check(_run(exe, workload, tmp_path), workload)
