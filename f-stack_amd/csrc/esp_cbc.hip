@@ -53,6 +53,15 @@ constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
 constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode == 6 ? 65536u : 163840u; }
 
+#ifndef ETA_PROBE_SHA1ONLY
+#define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
+#endif
+#ifndef ETA_U
+#define ETA_U 4              // blocks per lane per pass of the block-parallel decrypt
+#endif
+#ifndef ETA_WG2
+#define ETA_WG2 768          // in-place verify-first launch (MODE 2, SHA-1 / SHA2-256 sessions)
+#endif
 #ifndef ETA_WG3
 #define ETA_WG3 768
 #endif
@@ -199,11 +208,11 @@ __device__ __forceinline__ uint4 aes_dec(uint4 in, KP dk, int nr, const uint8_t 
 
 // Four independent blocks through the same rounds: 64 table reads in flight
 // per lane per round instead of 16 (the decrypt of one 64-byte HMAC chunk).
-template <typename KP>
-__device__ __forceinline__ void aes_dec4(uint4 (&v)[4], KP dk, int nr, const uint8_t *lds, uint32_t slot) {
-  uint32_t s[4][4];
+template <int N, typename KP>
+__device__ __forceinline__ void aes_dec4(uint4 (&v)[N], KP dk, int nr, const uint8_t *lds, uint32_t slot) {
+  uint32_t s[N][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < N; ++q) {
     s[q][0] = bswap32(v[q].x) ^ dk[0];
     s[q][1] = bswap32(v[q].y) ^ dk[1];
     s[q][2] = bswap32(v[q].z) ^ dk[2];
@@ -214,7 +223,7 @@ __device__ __forceinline__ void aes_dec4(uint4 (&v)[4], KP dk, int nr, const uin
     const uint32_t k0 = ror16(dk[4 * r]), k1 = ror16(dk[4 * r + 1]);
     const uint32_t k2 = ror16(dk[4 * r + 2]), k3 = ror16(dk[4 * r + 3]);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < N; ++q) {
       const uint32_t s0 = s[q][0], s1 = s[q][1], s2 = s[q][2], s3 = s[q][3];
       const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s3, slot, 2));
       const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s1, slot, 0));
@@ -233,7 +242,7 @@ __device__ __forceinline__ void aes_dec4(uint4 (&v)[4], KP dk, int nr, const uin
   const uint32_t *si = reinterpret_cast<const uint32_t *>(lds + LDS_SI);
   const uint32_t ls = slot >> 2;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < N; ++q) {
     uint32_t o[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -284,11 +293,11 @@ __device__ __forceinline__ uint4 aes_enc(uint4 in, KP ek, int nr, const uint8_t 
 
 // Four independent blocks through the encryption rounds (CTR keystream of
 // one 64-byte chunk): Te0/Te1 at `lds`, round keys `ek` (enc schedule).
-template <typename KP>
-__device__ __forceinline__ void aes_enc4(uint4 (&v)[4], KP ek, int nr, const uint8_t *lds, uint32_t slot) {
-  uint32_t s[4][4];
+template <int N, typename KP>
+__device__ __forceinline__ void aes_enc4(uint4 (&v)[N], KP ek, int nr, const uint8_t *lds, uint32_t slot) {
+  uint32_t s[N][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < N; ++q) {
     s[q][0] = bswap32(v[q].x) ^ ek[0];
     s[q][1] = bswap32(v[q].y) ^ ek[1];
     s[q][2] = bswap32(v[q].z) ^ ek[2];
@@ -299,7 +308,7 @@ __device__ __forceinline__ void aes_enc4(uint4 (&v)[4], KP ek, int nr, const uin
     const uint32_t k0 = ror16(ek[4 * r]), k1 = ror16(ek[4 * r + 1]);
     const uint32_t k2 = ror16(ek[4 * r + 2]), k3 = ror16(ek[4 * r + 3]);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < N; ++q) {
       const uint32_t s0 = s[q][0], s1 = s[q][1], s2 = s[q][2], s3 = s[q][3];
       const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s1, slot, 2));
       const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s3, slot, 0));
@@ -316,7 +325,7 @@ __device__ __forceinline__ void aes_enc4(uint4 (&v)[4], KP ek, int nr, const uin
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < N; ++q) {
     uint32_t o[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -356,7 +365,12 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
       f = xor3(b, c, d);
       k = 0xca62c1d6u;
     }
-    const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+    // e + K + W_t does not depend on a: summed first (and materialized, so
+    // the adds are not reassociated), the round's critical path is a ->
+    // {rotl 5, f} -> one add3 instead of a -> f -> add3 -> add3
+    uint32_t ekw = e + k + wt;
+    asm volatile("" : "+v"(ekw));
+    const uint32_t tmp = rotl(a, 5) + f + ekw;
     e = d;
     d = c;
     c = rotl(b, 30);
@@ -392,12 +406,18 @@ __device__ __forceinline__ void sha256_compress(uint32_t h[8], uint32_t w[16]) {
       wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
       w[t & 15] = wt;
     }
+    // h + K_t + W_t (and d + that) do not depend on this round's e or a:
+    // summed first, so e' = S1 + ch + (d+h+K+W) and t1 are one add3 each
+    uint32_t hkw = hh + kK256[t] + wt;
+    asm volatile("" : "+v"(hkw));
+    uint32_t dhkw = d + hkw;
+    asm volatile("" : "+v"(dhkw));
     const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
     const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);     // (e & f) | (~e & g)
-    const uint32_t t1 = hh + S1 + ch + kK256[t] + wt;
+    const uint32_t t1 = S1 + ch + hkw;
     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
     const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);     // majority
-    hh = g; g = f; f = e; e = d + t1;
+    hh = g; g = f; f = e; e = S1 + ch + dhkw;
     d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
@@ -1104,7 +1124,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
           if (MODE == 6 || CKS == CK_NARROW) {   // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
-            if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+            if (!ETA_PROBE_SHA1ONLY && s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
               hmac_t<HS_SHA256>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
                                 kp(s->opad), dg);
             else
@@ -1284,7 +1304,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       const int nr = (int)s->nr;
       // U blocks per lane per pass, 64 apart (each load instruction covers
       // 64 consecutive blocks), decrypted together for ILP
-      constexpr int U = 4;
+      constexpr int U = ETA_U;
       for (int base = total - 64 * U; base > -64 * U; base -= 64 * U) {
         int fk[U];
         uint32_t ik[U], rok[U], rplk[U], rdik[U], rsk[U];
@@ -1459,7 +1479,7 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
       if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
       return hipGetLastError() == hipSuccess ? 0 : -1;
 #endif
-      hipLaunchKernelGGL((eta_kernel<2, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+      hipLaunchKernelGGL((eta_kernel<2, ETA_WG2, CK_NARROW>), dim3(clamp(grid, ETA_WG2)), dim3(ETA_WG2), 0, st, p);
       if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
 #ifdef ESPGPU_VARIANTS
     } else if (fused == 4 && aux) {

@@ -624,6 +624,28 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 
+// The Horner multiplier's 8-bit table (value-major, entry (v, q) at v*256 +
+// q*16) built in LDS from the same power's 4-bit table in gtab (nibble
+// position j, value n at j*256 + n*16; host_crypto.cpp ghash_tables).  The
+// multiply is GF(2)-linear in the block, so T8[v][q] = T4[2q][v & 15] ^
+// T4[2q+1][v >> 4]: a workgroup that changes session reads 8 KiB (which the
+// final multiply's gathers share) instead of copying the 64-KiB table.  The
+// reference precomputes its tables once per key (gmac.c:48-63 -> gfmult.c:87
+// gf128_genmultable4); here the 8-bit expansion is redone per workgroup.
+template <int WG>
+__device__ __forceinline__ void stage_h8(uint8_t *dst, const uint8_t *t4, int tid) {
+#pragma unroll 1     // (unrolled, the allocator spills more in the record loop)
+  for (int k = 0; k < (4096 + WG - 1) / WG; ++k) {
+    const int e = tid + k * WG;
+    if (4096 % WG == 0 || e < 4096) {
+      const int q = e & 15, v = e >> 4;
+      const uint4 lo = *reinterpret_cast<const uint4 *>(t4 + (2 * q) * 256 + (v & 15) * 16);
+      const uint4 hi = *reinterpret_cast<const uint4 *>(t4 + (2 * q + 1) * 256 + (v >> 4) * 16);
+      *reinterpret_cast<uint4 *>(dst + e * 16) = xor4(lo, hi);
+    }
+  }
+}
+
 // ---- one 8-record group per wave -----------------------------------------------
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
@@ -1406,7 +1428,6 @@ template <int KIND, int DIR, int WG, int S>
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GCM_SPLIT_WPE)))
 void gcm_split_kernel(GcmParams p) {
   constexpr int RPW = 64 / S;
-  constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
   __shared__ __attribute__((aligned(16))) uint8_t lds[65536];
   const int tid = threadIdx.x;
   if (KIND == 0) {
@@ -1447,12 +1468,8 @@ void gcm_split_kernel(GcmParams p) {
         flags = sp->flags;
         mlen = sp->mlen;
         mode = sp->mode;
-        if (KIND == 1 && mode == ESPGPU_CSP_MODE_AEAD) {
-          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + gh8);
-          uint4 *dst = reinterpret_cast<uint4 *>(lds);
-#pragma unroll 4
-          for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
-        }
+        if (KIND == 1 && mode == ESPGPU_CSP_MODE_AEAD)
+          stage_h8<WG>(lds, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
       } else {
         mode = 0;
       }
@@ -1535,7 +1552,6 @@ template <int MODE, int WG, int S, bool STAGE = false>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   static_assert(S == kGcmLanesPerRec || S == kGcmLanesSmall, "GHASH tables exist for these strides");
   constexpr int RPW = 64 / S;             // records per wave
-  constexpr uint32_t gh8 = S == kGcmLanesPerRec ? kGh8Off : kGh8SmallOff;
   // the output ring (do_group): the headline decrypt's shape only
   constexpr bool RING = GCM_RING && MODE == 0 && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
   constexpr bool FM = GCM_FMUL_LDS && !RING && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
@@ -1603,10 +1619,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
           GCM_PHASE(1, true);
         }
         if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
-          const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + gh8);
-          uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
-#pragma unroll 4
-          for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
+          stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
           if (FM && !implicit) {
             // H^1..H^3 (power index i = 0..2): position-major in gtab (j*256 +
             // n*16), value-major here (n*512 + j*16)
@@ -1722,12 +1735,8 @@ __device__ __forceinline__ void burst_chunk(const GcmParams &p, uint8_t *lds, ui
       ss.flags = s->flags;
       ss.mlen = s->mlen;
       ss.mode = s->mode;
-      if (ss.mode == ESPGPU_CSP_MODE_AEAD) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes + kGh8SmallOff);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds + LDS_GT);
-#pragma unroll 4
-        for (int q = tid; q < (int)(kGh8Bytes / 16); q += WG) dst[q] = src[q];
-      }
+      if (ss.mode == ESPGPU_CSP_MODE_AEAD)    // H^8 (power index 7)
+        stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid);
     } else {
       ss.mode = 0;
     }

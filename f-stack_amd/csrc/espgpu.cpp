@@ -922,7 +922,7 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
     uint8_t zero[16] = {0}, h[16];
     hc::aes_encrypt_block(rk, nr, zero, h);       // H = E_K(0^128), gmac.c:56-60
     std::vector<uint8_t> tabs(kGhTableBytes);
-    hc::ghash_tables(h, kGcmLanesPerRec, tabs.data());
+    hc::ghash_tables(h, tabs.data());
     HIPCHK(c, hipMemcpy(c->d_gtab + (size_t)slot * kGhTableBytes, tabs.data(), kGhTableBytes, hipMemcpyHostToDevice));
   } else {
     const bool auth = csp->csp_mode == ESPGPU_CSP_MODE_ETA;

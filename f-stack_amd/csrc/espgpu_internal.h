@@ -38,17 +38,13 @@ struct DevSA {
 static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 
 // GHASH multiplication tables for one SA (host_crypto.cpp ghash_tables):
-// [0, 64 KiB)          H^1..H^8 with 4-bit indices, 8 KiB per power (power e
-//                      at (e-1)*8 KiB): nibble position j (byte j>>1 of the
-//                      block in memory order, low nibble if j even), value n
-//                      at j*256 + n*16; read from L2 by the per-record final
-//                      multiply by H^(8-l);
-// [kGh8Off, +64 KiB)   H^S with 8-bit indices (S = kGcmLanesPerRec): byte
-//                      position p, value v at v*256 + p*16 (value-major, so
-//                      a row's 16 positions sit in the 16 bank quads; staged
-//                      into LDS, the Horner multiplier, esp_gcm.hip gf_mul8).
-// [kGh8SmallOff, +64 KiB) the same for H^8: the Horner multiplier of the
-//                      small-batch kernel (kGcmLanesSmall lanes per record).
+// H^1..H^8 with 4-bit indices, 8 KiB per power (power e at (e-1)*8 KiB):
+// nibble position j (byte j>>1 of the block in memory order, low nibble if j
+// even), value n at j*256 + n*16.  Read from L2 by the per-record final
+// multiply by H^(S-l), and expanded by a workgroup into the 8-bit table of
+// its Horner multiplier H^S in LDS (esp_gcm.hip stage_h8: byte position p,
+// value v at v*256 + p*16, value-major so a row's 16 positions sit in the 16
+// bank quads; gf_mul8) whenever it changes session.
 // The measured-slower designs (GCM split / bitsliced, ETA MODE 0 / 5+6 / 7)
 // are compiled only into the variants library (-DESPGPU_VARIANTS).
 #ifdef ESPGPU_VARIANTS
@@ -60,10 +56,8 @@ constexpr int kGcmLanesPerRec = 4;                               // GCM kernel: 
 constexpr int kGcmLanesSmall = 8;                                // small batches: shorter serial chain
 constexpr uint32_t kGcmSmallBatch = 32768;                       // records: below, 8 lanes per record still fit the chip
 constexpr uint32_t kGhPowerBytes = 32 * 16 * 16;                 // 8192
-constexpr uint32_t kGh8Off = 8 * kGhPowerBytes;
-constexpr uint32_t kGh8Bytes = 16 * 256 * 16;                    // 65536
-constexpr uint32_t kGh8SmallOff = kGh8Off + kGh8Bytes;
-constexpr uint32_t kGhTableBytes = kGh8SmallOff + kGh8Bytes;     // 196608
+constexpr uint32_t kGh8Bytes = 16 * 256 * 16;                    // 65536: an 8-bit table (LDS only)
+constexpr uint32_t kGhTableBytes = 8 * kGhPowerBytes;            // 65536 per SA
 
 // A chunk: up to kChunkRecs records of ONE session, processed by one
 // workgroup iteration of the GCM kernel.  rec positions index `order`

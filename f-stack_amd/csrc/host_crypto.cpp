@@ -152,15 +152,11 @@ void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
   }
 }
 
-void ghash_tables(const uint8_t h[16], int stride, uint8_t *out) {
-  // Section 1 (64 KiB): powers H^1..H^8 (index 0..7) with 4-bit indices:
-  //   power p, nibble position j (byte j>>1, low nibble if j even), value n
-  //   at p*8192 + j*256 + n*16 = (the block whose nibble j is n) * H^(p+1).
-  // Section 3 (at 128 KiB): H^8 with 8-bit indices, the same layout.
-  // Section 2 (at 64 KiB): H^S with 8-bit indices (S = kGcmLanesPerRec, the
-  //   GCM kernel's Horner stride): byte position q, value v at v*256 + q*16
-  //   = (the block whose byte q is v) * H^S.  Value-major: the 16 positions
-  //   of one value fill one 256-byte LDS row, one position per bank quad.
+void ghash_tables(const uint8_t h[16], uint8_t *out) {
+  // H^1..H^8 (index 0..7) with 4-bit indices: power p, nibble position j
+  // (byte j>>1, low nibble if j even), value n at p*8192 + j*256 + n*16 =
+  // (the block whose nibble j is n) * H^(p+1).  The kernels' 8-bit Horner
+  // tables are expanded from these on the device (ghash_expand8).
   uint8_t pw[8][16];
   memcpy(pw[0], h, 16);
   for (int p = 1; p < 8; ++p) gf128_mul(pw[p - 1], h, pw[p]);
@@ -183,18 +179,17 @@ void ghash_tables(const uint8_t h[16], int stride, uint8_t *out) {
       }
     }
   }
-  // the 8-bit H^S table (and after it the 8-bit H^8 table of the
-  // small-batch kernel) from the 4-bit ones (GF(2)-linear in the block)
-  for (int sec = 0; sec < 2; ++sec) {
-    const uint8_t *h8 = out + (size_t)((sec ? 8 : stride) - 1) * 8192;
-    uint8_t *t8 = out + (8 + 8 * sec) * 8192;
-    for (int q = 0; q < 16; ++q)
-      for (int v = 0; v < 256; ++v) {
-        const uint8_t *lo = h8 + (2 * q) * 256 + (v & 15) * 16;
-        const uint8_t *hi = h8 + (2 * q + 1) * 256 + (v >> 4) * 16;
-        for (int k = 0; k < 16; ++k) t8[(size_t)v * 256 + (size_t)q * 16 + k] = lo[k] ^ hi[k];
-      }
-  }
+}
+
+void ghash_expand8(const uint8_t *t4, uint8_t *t8) {
+  // the multiply is GF(2)-linear in the block: byte q = v contributes the
+  // low nibble's product plus the high nibble's (esp_gcm.hip stage_h8)
+  for (int q = 0; q < 16; ++q)
+    for (int v = 0; v < 256; ++v) {
+      const uint8_t *lo = t4 + (2 * q) * 256 + (v & 15) * 16;
+      const uint8_t *hi = t4 + (2 * q + 1) * 256 + (v >> 4) * 16;
+      for (int k = 0; k < 16; ++k) t8[(size_t)v * 256 + (size_t)q * 16 + k] = lo[k] ^ hi[k];
+    }
 }
 
 void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {

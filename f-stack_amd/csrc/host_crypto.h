@@ -24,10 +24,12 @@ void aes_encrypt_block(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t
 // GF(2^128) product in GCM bit order (SP 800-38D Algorithm 1).
 void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
 
-// GHASH table set for the GCM kernel (kGhTableBytes, espgpu_internal.h):
-// H^1..H^8 with 4-bit indices (8 KiB each), then H^stride with 8-bit
-// indices (64 KiB); stride = the kernel's lanes per record (1..8).
-void ghash_tables(const uint8_t h[16], int stride, uint8_t *out);
+// GHASH table set for the GCM kernels (kGhTableBytes, espgpu_internal.h):
+// H^1..H^8 with 4-bit indices (8 KiB each).
+void ghash_tables(const uint8_t h[16], uint8_t *out);
+// The 8-bit table (64 KiB, value-major) of the power whose 4-bit table is t4:
+// what esp_gcm.hip stage_h8 builds in LDS (host mirror for the self-test).
+void ghash_expand8(const uint8_t *t4, uint8_t *t8);
 
 // SHA-1 compression of one 64-byte block into state h[5].
 void sha1_compress(uint32_t h[5], const uint8_t block[64]);

@@ -7,18 +7,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_ghash_table_layout_selftest(tmp_path):
-    """The 8-bit H^4 and H^8 (LDS) and 4-bit H^1..H^8 (global) GHASH tables
-    the GCM kernels index, and their stride-4 / stride-8 Horner + final
+    """The 4-bit H^1..H^8 (global) GHASH tables, the 8-bit H^4 and H^8 tables
+    the GCM kernels expand from them in LDS (stage_h8 / ghash_expand8), and their stride-4 / stride-8 Horner + final
     H^(S-l) combination,
     against gf128_mul and a serial GHASH (tools/ghash_selftest.cpp)."""
     import re
     hdr = open(os.path.join(ROOT, "f-stack_amd", "csrc", "espgpu_internal.h")).read()
     # the self-test mirrors these constants; keep them in step with the header
     assert re.search(r"kGhPowerBytes = 32 \* 16 \* 16;", hdr)
-    assert re.search(r"kGh8Off = 8 \* kGhPowerBytes;", hdr)
     assert re.search(r"kGh8Bytes = 16 \* 256 \* 16;", hdr)
-    assert re.search(r"kGh8SmallOff = kGh8Off \+ kGh8Bytes;", hdr)
-    assert re.search(r"kGhTableBytes = kGh8SmallOff \+ kGh8Bytes;", hdr)
+    assert re.search(r"kGhTableBytes = 8 \* kGhPowerBytes;", hdr)
     assert re.search(r"kGcmLanesPerRec = 4;", hdr) and re.search(r"kGcmLanesSmall = 8;", hdr)
     exe = tmp_path / "ghash_selftest"
     csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
