@@ -49,9 +49,7 @@
 #include <algorithm>
 
 #include "espgpu_internal.h"
-#ifdef ESPGPU_VARIANTS
 #include "aes_bs.h"
-#endif
 #include "xfer_copy.h"
 
 // Experiment switches (tools/variant.sh builds; defaults are the product)
@@ -102,6 +100,16 @@
 #ifndef GCM_FMUL_LDS
 #define GCM_FMUL_LDS 0
 #endif
+// Hybrid AES (throughput kernel, AES-128): every GCM_HYBRID-th interior pair
+// step's 8 counter blocks of a record are computed by the record's 4 lanes
+// bitsliced on the VALU (aes_ctr8_bsq) instead of by T-table lookups on the
+// LDS pipe, which bounds the kernel; 0 = T-tables only.
+#ifndef GCM_HYBRID
+#define GCM_HYBRID 0
+#endif
+#ifndef GCM_HYBRID_PRIO
+#define GCM_HYBRID_PRIO 0
+#endif
 
 namespace espgpu {
 
@@ -119,6 +127,10 @@ constexpr uint32_t kFmBytes = 3 * kGhPowerBytes;
 // flight, 256 records per workgroup = the 32 KiB the tables leave of 160 KiB.
 constexpr uint32_t LDS_RING = LDS_BYTES;
 constexpr uint32_t kRingBytes = 128 * 256;
+// GCM_HYBRID: the session's round keys 1..10 as bit planes, [round][row][plane]
+constexpr uint32_t LDS_KP = LDS_BYTES;
+constexpr uint32_t kKpBytes = 10 * 4 * 8 * 4;
+constexpr int kHyb = GCM_HYBRID > 0 ? GCM_HYBRID : 1;   // one pair step in kHyb is bitsliced
 
 // Round keys are read through the constant address space: uniform loads from
 // it become s_load (SGPRs, scalar cache) instead of vector loads or LDS reads.
@@ -468,6 +480,143 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32
   }
 }
 
+// ---- quad-bitsliced AES-CTR on the VALU (GCM_HYBRID) ------------------------
+// The T-table rounds cost the LDS pipe 16 lookups per block-round; bitsliced
+// rounds cost only VALU issue, which the T-table kernel leaves two-thirds idle.
+// The 4 lanes of a record (a quad) encrypt the 8 counter blocks of one pair
+// step together: lane q holds row q of the 8 states as 8 bit planes (bit
+// 8c + b of plane i = bit i of state byte (q, c) of block b), so a lane's
+// S-box is aes_bs.h's circuit on 8 registers (S' = S ^ 0x63, the round keys
+// are DevSA::dk's K_r ^ 0x63..), ShiftRows rotates each plane right by 8q,
+// and MixColumns takes rows q+1 and q+2 from the other lanes of the quad by
+// DPP quad_perm (the VALU's own operand crossbar: no LDS).  Round keys are
+// bit planes in LDS (2 ds_read_b128 per lane and round for 8 blocks).  The
+// keystream leaves as the T-table path's: lane q gets blocks q and q + 4 (AES
+// slots 4a + q and 4a + 4 + q) as memory-order words.  Host model, checked
+// against the table AES: tools/bsq_selftest.cpp.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t x) {
+  // (bound_ctrl on: quad_perm never reads outside the quad, and it lets the
+  // DPP move fold into the consuming VALU instruction)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
+}
+constexpr int kQpRot1 = 0x39;   // quad_perm [1,2,3,0]: lane q reads lane q+1
+constexpr int kQpXor2 = 0x4E;   // quad_perm [2,3,0,1]: lane q reads lane q^2 (= q+2)
+constexpr int kQpXor1 = 0xB1;   // quad_perm [1,0,3,2]: lane q reads lane q^1
+
+// bit i (within each byte) of a[s] <- bit s of a[i]: planes <-> per-block words
+__device__ __forceinline__ void bsq_transpose8(uint32_t (&a)[8]) {
+  constexpr uint32_t M[3] = {0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int j = 4 >> q;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k & j) continue;
+      const uint32_t t = __builtin_amdgcn_bitop3_b32(a[k] >> j, a[k + j], M[q], 0x28);   // (x ^ y) & m
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
+}
+
+// The session's round keys 1..10 as bit planes into LDS (at a session change):
+// word [r-1][q][i], byte c = bit i of key byte (q, c) of K'_r = byte q of dk[4r + c].
+template <int WG>
+__device__ __forceinline__ void stage_kp(uint8_t *dst, rkptr dk, int tid) {
+  for (int t = tid; t < 320; t += WG) {
+    const int r = (t >> 5) + 1, q = (t >> 3) & 3, i = t & 7;
+    uint32_t w = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w |= (((dk[4 * r + c] >> (8 * q + i)) & 1u) * 0xffu) << (8 * c);
+    reinterpret_cast<uint32_t *>(dst)[t] = w;
+  }
+}
+
+// E_K(nonce || ctr0 + b), b = 0..7, AES-128: ka = block q, kb = block q + 4.
+// R: the lane's row of the three nonce columns entering round 1 (byte c =
+// state byte (q, c), c < 3; bswap'd s0c..s2c); rk3: round-0 key word of
+// column 3 (big-endian); qs = 8q; qb0 / qb1: bits 0 / 1 of q.  Every lane of
+// the wave must be active (DPP reads the quad's other lanes).
+__device__ __forceinline__ void aes_ctr8_bsq(uint32_t R, uint32_t ctr0, uint32_t rk3, uint32_t qs, bool qb0,
+                                             bool qb1, const uint8_t *lds, uint4 &ka, uint4 &kb) {
+  // VALU-only work: issue priority below the T-table steps of the other
+  // waves, whose lookups keep the LDS pipe busy (GCM_HYBRID_PRIO)
+  if (GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(0);
+  uint32_t P[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) P[b] = R | ((((ctr0 + (uint32_t)b) ^ rk3) << qs) & 0xff000000u);
+  bsq_transpose8(P);
+  const uint8_t *kp = lds + LDS_KP + qs * 4;            // row q's planes of round 1
+#pragma unroll 1
+  for (int r = 0; r < 10; ++r) {
+    bs::sbox(P, 0u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) P[i] = __builtin_amdgcn_alignbit(P[i], P[i], qs);   // ShiftRows
+    if (r < 9) {
+      // out_q = xtime(s_q ^ s_q+1) ^ (s_q ^ s_q+1 ^ s_q+2 ^ s_q+3) ^ s_q
+      uint32_t t[8], u[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = P[i] ^ qperm<kQpRot1>(P[i]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) u[i] = t[i] ^ qperm<kQpXor2>(t[i]);
+      const uint32_t h = t[7];
+      P[0] = bs::x3(h, u[0], P[0]);
+      P[1] = bs::x3(bs::x3(t[0], h, u[1]), P[1], 0u);
+      P[2] = bs::x3(t[1], u[2], P[2]);
+      P[3] = bs::x3(bs::x3(t[2], h, u[3]), P[3], 0u);
+      P[4] = bs::x3(bs::x3(t[3], h, u[4]), P[4], 0u);
+      P[5] = bs::x3(t[4], u[5], P[5]);
+      P[6] = bs::x3(t[5], u[6], P[6]);
+      P[7] = bs::x3(t[6], u[7], P[7]);
+    }
+    const uint4 k0 = *reinterpret_cast<const uint4 *>(kp + r * 128);
+    const uint4 k1 = *reinterpret_cast<const uint4 *>(kp + r * 128 + 16);
+    P[0] ^= k0.x, P[1] ^= k0.y, P[2] ^= k0.z, P[3] ^= k0.w;
+    P[4] ^= k1.x, P[5] ^= k1.y, P[6] ^= k1.z, P[7] ^= k1.w;
+  }
+  bsq_transpose8(P);                                   // P[b]: byte c = keystream byte (q, c) of block b
+  // 4x4 word transposes across the quad (blocks 0..3 and 4..7): lane q then
+  // holds rows 0..3 of blocks q and q + 4
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (b & 2) continue;
+      const int x0 = 4 * h + b, x1 = x0 + 2;
+      const uint32_t y = qperm<kQpXor2>(qb1 ? P[x0] : P[x1]);
+      P[x0] = qb1 ? y : P[x0];
+      P[x1] = qb1 ? P[x1] : y;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (b & 1) continue;
+      const int x0 = 4 * h + b, x1 = x0 + 1;
+      const uint32_t y = qperm<kQpXor1>(qb0 ? P[x0] : P[x1]);
+      P[x0] = qb0 ? y : P[x0];
+      P[x1] = qb0 ? P[x1] : y;
+    }
+  }
+  // rows -> memory-order column words
+  uint32_t C[8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t *X = P + 4 * h;
+    const uint32_t T0 = perm(X[1], X[0], 0x05010400u), T1 = perm(X[1], X[0], 0x07030602u);
+    const uint32_t T2 = perm(X[3], X[2], 0x05010400u), T3 = perm(X[3], X[2], 0x07030602u);
+    C[4 * h + 0] = perm(T2, T0, 0x05040100u);
+    C[4 * h + 1] = perm(T2, T0, 0x07060302u);
+    C[4 * h + 2] = perm(T3, T1, 0x05040100u);
+    C[4 * h + 3] = perm(T3, T1, 0x07060302u);
+  }
+  ka = make_uint4(C[0], C[1], C[2], C[3]);
+  kb = make_uint4(C[4], C[5], C[6], C[7]);
+  if (GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(1);
+}
+
 // ---- GHASH multiply by a fixed power (gf_mul, gfmult.c:219-229) ----------
 // Y * H^S with 8-bit tables in LDS: 16 lookups, one per byte position p, of the
 // 16-byte product (the block whose byte p is v) * H^S, XOR-accumulated.
@@ -654,7 +803,7 @@ __device__ __forceinline__ void stage_h8(uint8_t *dst, const uint8_t *t4, int ti
 //         itself, then a failed record's keystream XORed over it again
 // Steps m, m+1 of a lane run together: 2 independent AES blocks, then
 // GHASH as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with the 8-bit table.
-template <int MODE, int S, bool RING = false, bool FM = false>
+template <int MODE, int S, bool RING = false, bool FM = false, bool HB = false>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
                                          uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk,
                                          bool fm = false) {
@@ -701,6 +850,14 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     return;
   }
   const uint32_t rk3 = rk[3];
+  // GCM_HYBRID: the lane's row (q = l) of the nonce columns entering round 1
+  const uint32_t qs = 8u * (uint32_t)(lane & 3);
+  const bool qb0 = (lane & 1) != 0, qb1 = (lane & 2) != 0;
+  uint32_t Rq = 0;
+  if (HB) {
+    const uint32_t sh = 24u - qs;
+    Rq = ((s0c >> sh) & 0xffu) | (((s1c >> sh) & 0xffu) << 8) | (((s2c >> sh) & 0xffu) << 16);
+  }
 #if GCM_OUTALIGN
   // layout probe (tools/outalign_ab.sh, bench.py --out-pad 40; cfg1's
   // 1500-byte slots only, results land elsewhere): record k's plaintext at
@@ -893,7 +1050,10 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
             Cb = ld16(rec + 16 + 16 * jb);
           }
           uint4 ka, kb;
-          aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+          if (HB && nr == 10 && (a >> 1) % kHyb == kHyb - 1)                  // wave-uniform
+            aes_ctr8_bsq(Rq, (uint32_t)(S * a) + 2u, rk3, qs, qb0, qb1, lds, ka, kb);
+          else
+            aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
           const uint4 Oa = xor4(Ca, ka), Ob = xor4(Cb, kb);
           if (RING) {
             ring_step(a, Oa, Ob);
@@ -1555,8 +1715,11 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // the output ring (do_group): the headline decrypt's shape only
   constexpr bool RING = GCM_RING && MODE == 0 && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
   constexpr bool FM = GCM_FMUL_LDS && !RING && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0) + (FM ? kFmBytes : 0)];
+  constexpr bool HB = GCM_HYBRID > 0 && !RING && !FM && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0) + (FM ? kFmBytes : 0) +
+                                                      (HB ? kKpBytes : 0)];
   const int tid = threadIdx.x;
+  if (HB && GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(1);
   GCM_PHASE(0, true);
   // The T-table (per entry 32 slots of Te0 then 32 slots of Te1, see tpa())
   // is filled with the first session's GHASH table: a workgroup that draws no
@@ -1620,6 +1783,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
           stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
+          if (HB && nr == 10) stage_kp<WG>(lds + LDS_KP, (rkptr)(const void *)(p.sas[sa].dk), tid);
           if (FM && !implicit) {
             // H^1..H^3 (power index i = 0..2): position-major in gtab (j*256 +
             // n*16), value-major here (n*512 + j*16)
@@ -1659,8 +1823,8 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         continue;
       }
-      do_group<MODE, S, RING, FM>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk),
-                                  !implicit);
+      do_group<MODE, S, RING, FM, HB>(p, lds, di, have, sa, flags, mlen, (int)nr,
+                                      (rkptr)(const void *)(p.sas[sa].rk), !implicit);
     }
     GCM_PHASE(5, it == 0);
     if (STAGE) {

@@ -42,3 +42,20 @@ def test_bitsliced_aes_selftest(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]
     assert r.stdout.startswith("OK")
+
+
+def test_quad_bitsliced_aes_selftest(tmp_path):
+    """The quad-bitsliced AES-128 counter step of the hybrid GCM switch
+    (esp_gcm.hip aes_ctr8_bsq, GCM_HYBRID: a record's 4 lanes hold one state
+    row each as bit planes, MixColumns across the quad), modelled lane by
+    lane on the CPU with aes_bs.h's S-box circuit and DevSA::dk's key form,
+    against host_crypto's table AES incl. counter runs that carry across
+    bytes (tools/bsq_selftest.cpp)."""
+    exe = tmp_path / "bsq_selftest"
+    csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
+                    os.path.join(ROOT, "tools", "bsq_selftest.cpp"),
+                    os.path.join(csrc, "host_crypto.cpp")], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert r.stdout.startswith("OK")
