@@ -1120,6 +1120,8 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         if (valid && MODE == 8) ok = true;          // decrypt every valid record (MODE 6 verifies beside it)
         if (valid && (MODE == 2 || MODE == 3 || MODE == 6 || MODE == 7) && s->aalg == 0) {
           ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
+        } else if (valid && (MODE == 2 || MODE == 3) && (eopts() & 0x10000)) {
+          ok = true;                                        // knob: no verify pass at all
         } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
@@ -1381,7 +1383,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
           v[k] = pv[k] = make_uint4(0, 0, 0, 0);
-          if (fk[k] >= 0) {
+          if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass loads
             const uint8_t *rec = p.arena + rok[k];
             if (null) {
               v[k] = ld16(rec + 8 + 16 * ik[k]);                                     // P_i = C_i
@@ -1398,12 +1400,12 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         if (null) {
         } else if (ctr) {
           aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
-        } else {
+        } else if (!(eopts() & 0x40000)) {                       // knob: no decrypt-pass AES
           aes_dec4(v, kp(s->dk), nr, lds, slot);
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-          if (fk[k] >= 0) {
+          if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass stores
             uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3 / 5 / 7: p.out (may be p.arena)
             const uint32_t i = ik[k], rpl = rplk[k];
             const int rem = (int)rpl - 16 * (int)i;
