@@ -56,6 +56,9 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_PROBE_SHA1ONLY
 #define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
 #endif
+#ifndef ETA_HMAC_QUAD
+#define ETA_HMAC_QUAD 0      // MODE 2 / 3 verify with quad-coalesced block loads (hmac_quad)
+#endif
 #ifndef ETA_U
 #define ETA_U 4              // blocks per lane per pass of the block-parallel decrypt
 #endif
@@ -536,6 +539,104 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
       for (int k = 0; k < 16; ++k) h[k & 7] ^= w[k];
     } else {
       Hash<HS>::compress(h, w);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = h[k];
+}
+
+// hmac_t for a whole wave whose lanes each verify one record (MODE 2 / 3,
+// ETA_HMAC_QUAD): the same hash, but a block's 64 bytes reach their lane by
+// a coalesced load.  Lane 4Q+k loads piece k (16 bytes) of block b of each of
+// the quad's 4 records, so one load instruction covers 16 records x 64
+// contiguous bytes (16 lines) instead of 64 records x 16 bytes (64 lines), and
+// a 4x4 transpose across the quad (DPP) hands each lane its record's pieces.
+// Every lane of the wave must call it (act = this lane's record is hashed);
+// the block loop runs to the wave's longest message.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
+}
+template <int I>
+__device__ __forceinline__ uint32_t qbcast(uint32_t x) { return qdpp<I * 0x55>(x); }   // quad_perm [I,I,I,I]
+
+// lane q of a quad: A[i] (i = 0..3) -> lane q holds, in A[k], lane k's A[q]
+__device__ __forceinline__ void quad_transpose4(uint32_t (&A)[4], bool qb0, bool qb1) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {                  // distance 2: pairs (0,2), (1,3)
+    const uint32_t y = qdpp<0x4E>(qb1 ? A[b] : A[b + 2]);
+    A[b] = qb1 ? y : A[b];
+    A[b + 2] = qb1 ? A[b + 2] : y;
+  }
+#pragma unroll
+  for (int b = 0; b < 4; b += 2) {               // distance 1: pairs (0,1), (2,3)
+    const uint32_t y = qdpp<0xB1>(qb0 ? A[b] : A[b + 1]);
+    A[b] = qb0 ? y : A[b];
+    A[b + 1] = qb0 ? A[b + 1] : y;
+  }
+}
+
+template <int HS>
+__device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi, kptr ipad,
+                          kptr opad, uint32_t out[8]) {
+  constexpr int W = Hash<HS>::W;
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  const uint32_t L = act ? L0 + (esn ? 4u : 0u) : 0u;
+  const uint32_t nfull = act ? L0 / 64 : 0u;
+  const uint32_t total = act ? (L + 9 + 63) / 64 : 0u;
+  const uint64_t bits = (uint64_t)(64 + L) * 8;
+  uint32_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = (act && k < W) ? ipad[k] : 0u;
+  // the quad's record pointers and full-block counts
+  const uint64_t rp = (uint64_t)(uintptr_t)rec;
+  const uint32_t rlo = (uint32_t)rp, rhi = (uint32_t)(rp >> 32);
+  const uint8_t *pr[4] = {
+      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<0>(rhi) << 32) | qbcast<0>(rlo)),
+      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<1>(rhi) << 32) | qbcast<1>(rlo)),
+      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<2>(rhi) << 32) | qbcast<2>(rlo)),
+      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<3>(rhi) << 32) | qbcast<3>(rlo))};
+  const uint32_t pn[4] = {qbcast<0>(nfull), qbcast<1>(nfull), qbcast<2>(nfull), qbcast<3>(nfull)};
+  uint32_t tw = total;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) tw = max(tw, (uint32_t)__shfl_xor((int)tw, o));
+  for (uint32_t b = 0; b <= tw; ++b) {            // wave-uniform trip count
+    uint4 P[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P[i] = b < pn[i] ? ld16(pr[i] + 64 * b + 16 * q) : make_uint4(0, 0, 0, 0);
+    uint32_t X[4] = {P[0].x, P[1].x, P[2].x, P[3].x}, Y[4] = {P[0].y, P[1].y, P[2].y, P[3].y};
+    uint32_t Z[4] = {P[0].z, P[1].z, P[2].z, P[3].z}, V[4] = {P[0].w, P[1].w, P[2].w, P[3].w};
+    quad_transpose4(X, qb0, qb1);
+    quad_transpose4(Y, qb0, qb1);
+    quad_transpose4(Z, qb0, qb1);
+    quad_transpose4(V, qb0, qb1);
+    uint32_t w[16];
+    if (b < nfull) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {             // piece k of this lane's record
+        w[4 * k] = bswap32(X[k]);
+        w[4 * k + 1] = bswap32(Y[k]);
+        w[4 * k + 2] = bswap32(Z[k]);
+        w[4 * k + 3] = bswap32(V[k]);
+      }
+    } else if (b < total) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
+    } else {
+      outer_block<HS>(h, w);
+      if (act) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) h[k] = opad[k];
+      }
+    }
+    if (b <= total) {
+      if (eopts() & 0x20000) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h[k & 7] ^= w[k];
+      } else {
+        Hash<HS>::compress(h, w);
+      }
     }
   }
 #pragma unroll
@@ -1084,6 +1185,9 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
     // ---- lane = record: descriptor, HMAC (verify or compute) ----
     bool valid = false, ok = false;
     uint32_t off = 0, len = 0, sa = 0, plen = 0, hl = 24, salt = 0, esnh = 0;
+    int hq = 0;                                  // ETA_HMAC_QUAD: 1 SHA-1 / 2 SHA2-256 record to hash
+    bool hq_esn = false;
+    uint32_t hq_mlen = 0;
     if (have) {
       const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
       off = dv.x * 4;
@@ -1127,6 +1231,10 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
         } else if (valid && (MODE == 2 || MODE == 3) && (eopts() & 0x10000)) {
           ok = true;                                        // knob: no verify pass at all
+        } else if (ETA_HMAC_QUAD && valid && (MODE == 2 || MODE == 3) && CKS == CK_NARROW) {
+          hq = s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 1;   // hashed below, by the whole wave
+          hq_esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
+          hq_mlen = mlen;
         } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
@@ -1145,6 +1253,27 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           for (uint32_t k = 0; k < mlen / 4; ++k)
             diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
           ok = diff == 0 || (eopts() & 0x20000);            // (knob: no compression, decrypt anyway)
+        }
+      }
+    }
+    if (ETA_HMAC_QUAD && (MODE == 2 || MODE == 3) && CKS == CK_NARROW) {
+      // the verify of this unit's records, the whole wave at once
+#pragma unroll
+      for (int hs = 1; hs <= 2; ++hs) {
+        if (!__any(hq == hs)) continue;           // wave-uniform
+        const bool act = hq == hs;
+        const DevSA *s = p.sas + (act ? sa : 0u);
+        const uint8_t *rec = p.arena + off;
+        uint32_t dg[16];
+        if (hs == 2)
+          hmac_quad<HS_SHA256>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
+        else
+          hmac_quad<HS_SHA1>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
+        if (act) {
+          uint32_t diff = 0;
+          for (uint32_t k = 0; k < hq_mlen / 4; ++k)
+            diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
+          ok = diff == 0 || (eopts() & 0x20000);
         }
       }
     }
