@@ -623,7 +623,7 @@ __device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, u
     } else if (b < total) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
-    } else {
+    } else if (b == total) {                     // (lanes past their total keep their digest)
       outer_block<HS>(h, w);
       if (act) {
 #pragma unroll
