@@ -56,8 +56,11 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_PROBE_SHA1ONLY
 #define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
 #endif
+#ifndef ETA_TICKET_PF
+#define ETA_TICKET_PF 0
+#endif
 #ifndef ETA_HMAC_QUAD
-#define ETA_HMAC_QUAD 0      // MODE 2 / 3 verify with quad-coalesced block loads (hmac_quad)
+#define ETA_HMAC_QUAD 0      // MODE 2 verify with quad-coalesced block loads (hmac_quad)
 #endif
 #ifndef ETA_U
 #define ETA_U 4              // blocks per lane per pass of the block-parallel decrypt
@@ -1167,11 +1170,16 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   const bool implicit = p.chunks == nullptr;
   const uint32_t u0 = implicit ? 0u : p.nchunks[0];
   const uint32_t u1 = implicit ? (p.n + 63) / 64 : p.nchunks[1];
+  // ETA_TICKET_PF: the next unit's ticket is drawn as soon as this one is
+  // known (its atomic returns while the wave works on this unit)
+  uint32_t next_t = 0;
+  if (ETA_TICKET_PF && lane == 0) next_t = atomicAdd(&p.queue[0], 1u);
   for (;;) {
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&p.queue[0], 1u);
+    if (lane == 0) t = ETA_TICKET_PF ? next_t : atomicAdd(&p.queue[0], 1u);
     const uint32_t u = u0 + __builtin_amdgcn_readfirstlane(t);
     if (u >= u1) break;
+    if (ETA_TICKET_PF && lane == 0) next_t = atomicAdd(&p.queue[0], 1u);
     uint32_t di = 0;
     bool have;
     if (implicit) {
@@ -1231,7 +1239,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
           ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
         } else if (valid && (MODE == 2 || MODE == 3) && (eopts() & 0x10000)) {
           ok = true;                                        // knob: no verify pass at all
-        } else if (ETA_HMAC_QUAD && valid && (MODE == 2 || MODE == 3) && CKS == CK_NARROW) {
+        } else if (ETA_HMAC_QUAD && valid && MODE == 2 && CKS == CK_NARROW) {
           hq = s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 1;   // hashed below, by the whole wave
           hq_esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
           hq_mlen = mlen;
@@ -1256,7 +1264,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
         }
       }
     }
-    if (ETA_HMAC_QUAD && (MODE == 2 || MODE == 3) && CKS == CK_NARROW) {
+    if (ETA_HMAC_QUAD && MODE == 2 && CKS == CK_NARROW) {
       // the verify of this unit's records, the whole wave at once
 #pragma unroll
       for (int hs = 1; hs <= 2; ++hs) {
