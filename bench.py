@@ -475,12 +475,13 @@ def launched_kernel(cfg, inplace):
     only), MODE 0 = out of place, S = 4 lanes per record (every bench
     config has >= 32K records: the small-batch S = 8 kernel is not launched),
     STAGE false (device-resident records);
-    eta_kernel<3 (out of place) / 2 (in place), 768, -2> for CBC + HMAC-SHA1
-    (verify pass, then the block-parallel decrypt of the verified records; -2 =
-    the launch for SHA-1 / SHA2-256 sessions, esp_cbc.hip CK_NARROW)."""
+    eta_kernel<3, 768, -2> (out of place) / <2, 1024, -2> (in place) for CBC +
+    HMAC-SHA1 (verify pass, then the block-parallel decrypt of the verified
+    records; -2 = the launch for SHA-1 / SHA2-256 sessions, esp_cbc.hip
+    CK_NARROW)."""
     if cfg["alg"] == "gcm":
         return "gcm_kernel<%d, 1024, 4, false>" % (3 if inplace else 0)
-    return "eta_kernel<2, 768, -2>" if inplace else "eta_kernel<3, 768, -2>"   # verify-first two-pass
+    return "eta_kernel<2, 1024, -2>" if inplace else "eta_kernel<3, 768, -2>"   # verify-first two-pass
 
 
 def profile_traffic(config, inplace, kernel, kern_ms):

@@ -56,17 +56,14 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_PROBE_SHA1ONLY
 #define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
 #endif
-#ifndef ETA_TICKET_PF
-#define ETA_TICKET_PF 0
-#endif
 #ifndef ETA_HMAC_QUAD
-#define ETA_HMAC_QUAD 0      // MODE 2 verify with quad-coalesced block loads (hmac_quad)
+#define ETA_HMAC_QUAD 1      // MODE 2 verify with quad-coalesced block loads (hmac_quad); 0: hmac_t
 #endif
 #ifndef ETA_U
 #define ETA_U 4              // blocks per lane per pass of the block-parallel decrypt
 #endif
 #ifndef ETA_WG2
-#define ETA_WG2 768          // in-place verify-first launch (MODE 2, SHA-1 / SHA2-256 sessions)
+#define ETA_WG2 1024         // in-place verify-first launch (MODE 2, SHA-1 / SHA2-256 sessions; 128 VGPRs with hmac_quad)
 #endif
 #ifndef ETA_WG3
 #define ETA_WG3 768
@@ -1170,16 +1167,11 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   const bool implicit = p.chunks == nullptr;
   const uint32_t u0 = implicit ? 0u : p.nchunks[0];
   const uint32_t u1 = implicit ? (p.n + 63) / 64 : p.nchunks[1];
-  // ETA_TICKET_PF: the next unit's ticket is drawn as soon as this one is
-  // known (its atomic returns while the wave works on this unit)
-  uint32_t next_t = 0;
-  if (ETA_TICKET_PF && lane == 0) next_t = atomicAdd(&p.queue[0], 1u);
   for (;;) {
     uint32_t t = 0;
-    if (lane == 0) t = ETA_TICKET_PF ? next_t : atomicAdd(&p.queue[0], 1u);
+    if (lane == 0) t = atomicAdd(&p.queue[0], 1u);
     const uint32_t u = u0 + __builtin_amdgcn_readfirstlane(t);
     if (u >= u1) break;
-    if (ETA_TICKET_PF && lane == 0) next_t = atomicAdd(&p.queue[0], 1u);
     uint32_t di = 0;
     bool have;
     if (implicit) {

@@ -107,9 +107,6 @@
 #ifndef GCM_HYBRID
 #define GCM_HYBRID 0
 #endif
-#ifndef GCM_TICKET_PF
-#define GCM_TICKET_PF 0
-#endif
 #ifndef GCM_HYBRID_PRIO
 #define GCM_HYBRID_PRIO 0
 #endif
@@ -1744,21 +1741,14 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // barrier keeps it until every wave has read it.
   __shared__ uint32_t s_ticket[RING ? 1 : 2];
   __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
-  // GCM_TICKET_PF: the next chunk's ticket is drawn as soon as this one is
-  // known, so its atomic (≈ 1-2 µs round trip to the one counter all
-  // workgroups share) is in flight during the chunk instead of in front of it
-  constexpr bool TPF = GCM_TICKET_PF && !RING;
-  uint32_t next_t = 0;
-  if (TPF && tid == 0) next_t = atomicAdd(&p.queue[0], 1u);
   for (uint32_t it = 0;; ++it) {
     uint32_t *tk = RING ? reinterpret_cast<uint32_t *>(lds + LDS_RING) : s_ticket + (it & 1);
-    if (tid == 0) *tk = TPF ? next_t : atomicAdd(&p.queue[0], 1u);
+    if (tid == 0) *tk = atomicAdd(&p.queue[0], 1u);
     __syncthreads();
     const uint32_t c = *tk;
     if (RING) __syncthreads();
     GCM_PHASE(2, it == 0);
     if (c >= nch) break;
-    if (TPF && tid == 0) next_t = atomicAdd(&p.queue[0], 1u);
     uint32_t sa, start, count;
     if (implicit) {
       start = c * p.chunk;
