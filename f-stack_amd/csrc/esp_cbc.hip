@@ -56,6 +56,15 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_PROBE_SHA1ONLY
 #define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
 #endif
+#ifndef ETA_STAGGER
+#define ETA_STAGGER 0        // probe: delay (s_memrealtime ticks) of the late-starting waves
+#endif
+#ifndef ETA_STAGGER_MODE
+#define ETA_STAGGER_MODE 0   // 0: odd waves start late; 1: wave w starts (w & 3) delays late
+#endif
+#ifndef ETA_XCDQ
+#define ETA_XCDQ 0           // per-XCD work-queue tickets (xcd_ticket)
+#endif
 #ifndef ETA_HMAC_QUAD
 #define ETA_HMAC_QUAD 1      // MODE 2 verify with quad-coalesced block loads (hmac_quad); 0: hmac_t
 #endif
@@ -1167,9 +1176,17 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   const bool implicit = p.chunks == nullptr;
   const uint32_t u0 = implicit ? 0u : p.nchunks[0];
   const uint32_t u1 = implicit ? (p.n + 63) / 64 : p.nchunks[1];
+  if (ETA_STAGGER && MODE == 2) {
+    // probe: start some waves late so the waves of a CU are not all in the
+    // same phase (verify: memory + VALU; decrypt: LDS) at the same time
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint64_t d = ETA_STAGGER_MODE ? (uint64_t)(w & 3) * ETA_STAGGER : (uint64_t)(w & 1) * ETA_STAGGER;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
+  }
   for (;;) {
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&p.queue[0], 1u);
+    if (lane == 0) t = ETA_XCDQ ? xcd_ticket(p.queue, blockIdx.x & 7u, u1 - u0) : atomicAdd(&p.queue[0], 1u);
     const uint32_t u = u0 + __builtin_amdgcn_readfirstlane(t);
     if (u >= u1) break;
     uint32_t di = 0;
@@ -1561,6 +1578,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
   // all have retired no ticket is drawn again: reset for the next launch.
   if (lane == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x * (WG / 64) - 1) {
     atomicExch(&p.queue[0], 0u);
+    if (ETA_XCDQ) xcd_reset(p.queue);
     atomicExch(&p.queue[1], 0u);
   }
 }

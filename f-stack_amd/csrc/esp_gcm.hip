@@ -85,6 +85,9 @@
 #ifndef GCM_RING
 #define GCM_RING 0
 #endif
+#ifndef GCM_XCDQ2
+#define GCM_XCDQ2 0  // per-XCD work-queue tickets (xcd_ticket) in gcm_kernel
+#endif
 // In-place decrypt, verify first (fused kernel, S = 4 and 8): 1 = one pass that decrypts
 // in place while hashing and rolls a failed record back (CTR is its own
 // inverse: the same keystream XORed over the plaintext restores the
@@ -1743,7 +1746,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
   for (uint32_t it = 0;; ++it) {
     uint32_t *tk = RING ? reinterpret_cast<uint32_t *>(lds + LDS_RING) : s_ticket + (it & 1);
-    if (tid == 0) *tk = atomicAdd(&p.queue[0], 1u);
+    if (tid == 0) *tk = GCM_XCDQ2 ? xcd_ticket(p.queue, blockIdx.x & 7u, nch) : atomicAdd(&p.queue[0], 1u);
     __syncthreads();
     const uint32_t c = *tk;
     if (RING) __syncthreads();
@@ -1851,6 +1854,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // so once all have retired no ticket is drawn again: reset for the next launch.
   if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
     atomicExch(&p.queue[0], 0u);
+    if (GCM_XCDQ2) xcd_reset(p.queue);
     atomicExch(&p.queue[1], 0u);
   }
 }

@@ -212,7 +212,7 @@ struct espgpu_ctx {
   uint8_t *d_gtab = nullptr;
   uint2 *d_tpair = nullptr, *d_dpair = nullptr;
   uint8_t *d_isbox = nullptr;
-  uint32_t *d_queue = nullptr;   // work queues: [0..1] GCM, [2..3] ETA (ticket, retired; self-resetting)
+  uint32_t *d_queue = nullptr;   // work-queue regions (kQueueRegionWords apart): GCM, ETA, ETA aux (self-resetting)
   std::vector<Session> sessions;
   std::vector<DevSA> h_sas;
   // ETA sessions: all, and by kernel: narrow-hash (SHA-1 / SHA2-256) CBC and
@@ -691,7 +691,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.order = p.order;
     q.chunks = p.chunks;
     q.nchunks = p.nchunks;
-    q.queue = c->d_queue + 2;
+    q.queue = c->d_queue + kQueueRegionWords;
     q.trailer = p.trailer;
     q.n = n;
     q.sas = c->d_sas;
@@ -704,7 +704,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
                    (c->n_wctr > 0 ? 8 : 0) | (c->n_whash > 0 ? 16 : 0);
     q.two_pass_all = c->eta_fused == 2 || c->eta_fused == 3;
     q.interleave = c->eta_fused == 3;
-    const EtaAux eaux{c->s_aux, c->ev_fork, c->ev_join, c->d_queue + 4};
+    const EtaAux eaux{c->s_aux, c->ev_fork, c->ev_join, c->d_queue + 2 * kQueueRegionWords};
     if (launch_eta(q, encrypt, ek, grid, c->eta_fused, st, &eaux))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
@@ -769,12 +769,12 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
         hipMalloc(&c->d_tpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_dpair, 256 * sizeof(uint2)) != hipSuccess ||
         hipMalloc(&c->d_isbox, 256) != hipSuccess ||
-        hipMalloc(&c->d_queue, 32) != hipSuccess) {
+        hipMalloc(&c->d_queue, 4 * kQueueRegionWords * 4) != hipSuccess) {
       rc = fail(c, ESPGPU_ENOMEM, "device SA table allocation failed");
       break;
     }
     hipMemset(c->d_sas, 0, (size_t)cfg.max_sessions * sizeof(DevSA));
-    hipMemset(c->d_queue, 0, 32);
+    hipMemset(c->d_queue, 0, 4 * kQueueRegionWords * 4);
     const hc::Tables &t = hc::tables();
     uint2 tp[256], dp[256];
     for (int x = 0; x < 256; ++x) {

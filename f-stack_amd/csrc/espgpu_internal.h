@@ -105,6 +105,34 @@ struct GcmParams {
   uint32_t out_stride;
 };
 
+// Work-queue regions (ctx d_queue): one per kernel family, kQueueRegionWords
+// apart.  Word 0 = the single ticket counter, word 1 = retired count; with
+// per-XCD queues (xcd_ticket) the 8 counters sit at kQueueXcdStride * (x + 1),
+// 256 bytes apart.
+constexpr uint32_t kQueueRegionWords = 1024;
+constexpr uint32_t kQueueXcdStride = 64;
+
+// Per-XCD tickets: a workgroup draws from the counter of its XCD (workgroups
+// are dispatched to the 8 XCDs round-robin: x = blockIdx.x & 7), ticket k of
+// counter x is unit x + 8k, so every XCD walks the same unit order (the
+// planner's largest first); a workgroup whose counter is exhausted tries the
+// other XCDs' in turn.  One device-scope counter serializes its atomics at
+// 12-14 ns each, eight at 2-2.4 ns (tools/atomicprobe.hip,
+// profiles/r5_eta_knobs_fm_atomics.txt).  Returns n when every counter is past
+// the end; the caller's last retiring workgroup / wave clears all eight.
+__device__ __forceinline__ uint32_t xcd_ticket(uint32_t *q, uint32_t x, uint32_t n) {
+  for (uint32_t j = 0; j < 8; ++j) {
+    const uint32_t xx = (x + j) & 7u;
+    const uint32_t k = atomicAdd(q + kQueueXcdStride * (xx + 1), 1u);
+    const uint32_t u = xx + 8u * k;
+    if (u < n) return u;
+  }
+  return n;
+}
+__device__ __forceinline__ void xcd_reset(uint32_t *q) {
+  for (uint32_t x = 0; x < 8; ++x) atomicExch(q + kQueueXcdStride * (x + 1), 0u);
+}
+
 struct EtaParams {
   uint8_t *arena;
   uint8_t *out;
