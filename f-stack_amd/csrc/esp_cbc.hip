@@ -56,6 +56,9 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_PROBE_SHA1ONLY
 #define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
 #endif
+#ifndef ETA_ENC_QUAD
+#define ETA_ENC_QUAD 1       // encrypt MAC pass (MODE 1): SHA-1 / SHA2-256 ICVs with hmac_quad
+#endif
 #ifndef ETA_STAGGER
 #define ETA_STAGGER 0        // probe: delay (s_memrealtime ticks) of the late-starting waves
 #endif
@@ -1300,10 +1303,21 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
       // lean kernel (no hash code, few VGPRs, 2 workgroups x 16 waves per
       // CU) where occupancy hides the round latency; CTR runs 4 blocks at a
       // time ----
-      if (have && valid) {
-        const DevSA *s = p.sas + sa;
-        uint8_t *rec = p.arena + off;
+      // One session at a time (a planner chunk has one): the session pointer
+      // is wave-uniform, so the round keys come through the scalar cache into
+      // SGPRs instead of a vector load per round on the CBC chain's critical
+      // path (per-lane keys: 2.87 ms for cfg3's 1M x 1496-B records)
+      bool run = have && valid;
+      uint64_t todo = __ballot(run);
+      while (todo) {
+        const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
+        const bool mine = run && sa == sau;
+        todo &= ~__ballot(mine);
+        run = run && !mine;
+        const DevSA *s = p.sas + sau;
         const int nr = (int)s->nr;
+        if (!mine) continue;
+        uint8_t *rec = p.arena + off;
         if (CKS == CK_CTR) {
           const uint32_t iv0 = *reinterpret_cast<const uint32_t *>(rec + 8);
           const uint32_t iv1 = *reinterpret_cast<const uint32_t *>(rec + 12);
@@ -1331,7 +1345,7 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               if (b + k < nb) {
-                prev = aes_enc(xor4(m[k], prev), s->rk, nr, lds, slot);
+                prev = aes_enc(xor4(m[k], prev), kp(s->rk), nr, lds, slot);
                 m[k] = prev;
               }
             }
@@ -1346,7 +1360,31 @@ __global__ __launch_bounds__(WG) void eta_kernel(EtaParams p) {
     if (MODE == 1) {
       // ---- encrypt, MAC pass (after MODE 4 wrote the ciphertext): HMAC over
       // SPI|SN|IV|CT (|ESN), ICV = its first mlen bytes ----
-      if (have && valid && p.sas[sa].aalg != 0) {           // CSP_MODE_CIPHER: no ICV
+      // SHA-1 / SHA2-256 ICVs with hmac_quad's coalesced block loads (the whole
+      // wave calls it), SHA2-384/512 with hmac_any
+      int hq1 = 0;
+      if (ETA_ENC_QUAD && have && valid) {
+        const uint32_t aa = p.sas[sa].aalg;
+        hq1 = aa == ESPGPU_CRYPTO_SHA1_HMAC ? 1 : aa == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 0;
+      }
+#pragma unroll
+      for (int hs = 1; hs <= 2; ++hs) {
+        if (!ETA_ENC_QUAD || !__any(hq1 == hs)) continue;     // wave-uniform
+        const bool act = hq1 == hs;
+        const DevSA *s = p.sas + (act ? sa : 0u);
+        uint8_t *rec = p.arena + off;
+        uint32_t dg[16];
+        if (hs == 2)
+          hmac_quad<HS_SHA256>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                               kp(s->opad), dg);
+        else
+          hmac_quad<HS_SHA1>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
+                             kp(s->opad), dg);
+        if (act)
+          for (uint32_t k = 0; k < s->mlen / 4; ++k)
+            *reinterpret_cast<uint32_t *>(rec + hl + plen + 4 * k) = bswap32(dg[k]);
+      }
+      if (have && valid && hq1 == 0 && p.sas[sa].aalg != 0) {   // CSP_MODE_CIPHER: no ICV
         const DevSA *s = p.sas + sa;
         uint8_t *rec = p.arena + off;
         uint32_t dg[16];
