@@ -59,15 +59,6 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_ENC_QUAD
 #define ETA_ENC_QUAD 1       // encrypt MAC pass (MODE 1): SHA-1 / SHA2-256 ICVs with hmac_quad
 #endif
-#ifndef ETA_ENC2
-#define ETA_ENC2 0           // probe (slower): encrypt, AES-CBC over planner chunks: eta_cbc_enc2_kernel (two chains per lane)
-#endif
-#ifndef ETA_ENC2_G
-#define ETA_ENC2_G 2         // eta_cbc_enc2_kernel: blocks per record per load / store
-#endif
-#ifndef ETA_ENC2_WPE
-#define ETA_ENC2_WPE 8       // eta_cbc_enc2_kernel: minimum waves per SIMD (launch bounds)
-#endif
 #ifndef ETA_ENC_QUAD4
 #define ETA_ENC_QUAD4 1      // MODE 4 CBC: cbc_enc_quad (quad-coalesced 64-byte groups)
 #endif
@@ -1711,190 +1702,6 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
 }
 
 
-// ---- ETA encrypt, AES-CBC cipher pass over planner chunks, two chains per lane
-// The CBC chain of a record is serial: MODE 4 (lane = record) has 16 table
-// reads in flight per lane per round and, at 8 waves per SIMD (the most two
-// 64-KiB-table workgroups allow), leaves the LDS pipe waiting on round
-// latency.  Here a wave takes two chunks and each lane encrypts one record of
-// each, the two chains interleaved round by round: twice the independent reads
-// per lane at the same occupancy.  Chunks hold one session each (the
-// planner's), so both schedules are wave-uniform and come by scalar loads.
-struct CbcRec {
-  uint8_t *rec;
-  uint32_t nb;        // payload blocks (0: nothing to do)
-};
-
-// lane's record of ETA chunk u, if it is an AES-CBC record of the chunk's
-// session with a valid payload (xform_esp.c:316-324); *sess = that session
-__device__ __forceinline__ CbcRec cbc_chunk_rec(const EtaParams &p, uint32_t u, int lane, uint32_t *sess,
-                                                bool *mixed) {
-  const Chunk ch = p.chunks[u];
-  const uint32_t sau = __builtin_amdgcn_readfirstlane(ch.sa);
-  *sess = sau;
-  CbcRec r{nullptr, 0};
-  bool other = false;
-  if ((uint32_t)lane < ch.count) {
-    const uint32_t di = p.order[ch.start + lane];
-    const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
-    const uint32_t len = dv.y & 0xffffu, sa = dv.y >> 16;
-    other = sa != sau;
-    const DevSA *s = sau < p.nsas ? p.sas + sau : nullptr;
-    if (!other && s && s->mode == ESPGPU_CSP_MODE_ETA && s->calg == ESPGPU_CRYPTO_AES_CBC) {
-      const int pl = (int)len - 24 - (int)s->mlen;
-      if (pl > 0 && (pl & 15) == 0 && (len & 3) == 0) {
-        r.rec = p.arena + dv.x * 4;
-        r.nb = (uint32_t)pl / 16;
-      }
-    }
-  }
-  *mixed = __any(other);
-  return r;
-}
-
-// two CBC blocks, one per chain, through the same rounds (Te0/Te1 at lds)
-__device__ __forceinline__ void aes_enc_x2(uint4 &x, uint4 &y, kptr ka, kptr kb, int nr, const uint8_t *lds,
-                                           uint32_t slot) {
-  uint32_t s[2][4] = {{bswap32(x.x) ^ ka[0], bswap32(x.y) ^ ka[1], bswap32(x.z) ^ ka[2], bswap32(x.w) ^ ka[3]},
-                      {bswap32(y.x) ^ kb[0], bswap32(y.y) ^ kb[1], bswap32(y.z) ^ kb[2], bswap32(y.w) ^ kb[3]}};
-#pragma unroll 1
-  for (int r = 1; r < nr; ++r) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const kptr ek = q ? kb : ka;
-      const uint32_t k0 = ror16(ek[4 * r]), k1 = ror16(ek[4 * r + 1]);
-      const uint32_t k2 = ror16(ek[4 * r + 2]), k3 = ror16(ek[4 * r + 3]);
-      const uint32_t s0 = s[q][0], s1 = s[q][1], s2 = s[q][2], s3 = s[q][3];
-      const uint32_t a0 = t0(lds, tpa(s0, slot, 3)), b0 = t1(lds, tpa(s1, slot, 2));
-      const uint32_t c0 = t0(lds, tpa(s2, slot, 1)), d0 = t1(lds, tpa(s3, slot, 0));
-      const uint32_t a1 = t0(lds, tpa(s1, slot, 3)), b1 = t1(lds, tpa(s2, slot, 2));
-      const uint32_t c1 = t0(lds, tpa(s3, slot, 1)), d1 = t1(lds, tpa(s0, slot, 0));
-      const uint32_t a2 = t0(lds, tpa(s2, slot, 3)), b2 = t1(lds, tpa(s3, slot, 2));
-      const uint32_t c2 = t0(lds, tpa(s0, slot, 1)), d2 = t1(lds, tpa(s1, slot, 0));
-      const uint32_t a3 = t0(lds, tpa(s3, slot, 3)), b3 = t1(lds, tpa(s0, slot, 2));
-      const uint32_t c3 = t0(lds, tpa(s1, slot, 1)), d3 = t1(lds, tpa(s2, slot, 0));
-      s[q][0] = xor3(a0, b0, ror16(xor3(c0, d0, k0)));
-      s[q][1] = xor3(a1, b1, ror16(xor3(c1, d1, k1)));
-      s[q][2] = xor3(a2, b2, ror16(xor3(c2, d2, k2)));
-      s[q][3] = xor3(a3, b3, ror16(xor3(c3, d3, k3)));
-    }
-  }
-  uint32_t o[2][4];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const kptr ek = q ? kb : ka;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint32_t a = t0(lds, tpa(s[q][c], slot, 3));
-      const uint32_t b = t0(lds, tpa(s[q][(c + 1) & 3], slot, 2));
-      const uint32_t cc = t0(lds, tpa(s[q][(c + 2) & 3], slot, 1));
-      const uint32_t d = t0(lds, tpa(s[q][(c + 3) & 3], slot, 0));
-      o[q][c] = xor3(perm(b, a, 0x0c0c0501u), perm(d, cc, 0x05010c0cu), bswap32(ek[4 * nr + c]));
-    }
-  }
-  x = make_uint4(o[0][0], o[0][1], o[0][2], o[0][3]);
-  y = make_uint4(o[1][0], o[1][1], o[1][2], o[1][3]);
-}
-
-// one chain (a chunk whose lanes are not all of its session, or a lone chunk):
-// MODE 4's loop, one session at a time
-__device__ __forceinline__ void cbc_chunk_single(const EtaParams &p, uint32_t u, int lane, const uint8_t *lds,
-                                                 uint32_t slot) {
-  const Chunk ch = p.chunks[u];
-  bool have = (uint32_t)lane < ch.count;
-  uint32_t off = 0, len = 0, sa = 0;
-  if (have) {
-    const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + p.order[ch.start + lane]);
-    off = dv.x * 4;
-    len = dv.y & 0xffffu;
-    sa = dv.y >> 16;
-    const DevSA *s = sa < p.nsas ? p.sas + sa : nullptr;
-    have = s && s->mode == ESPGPU_CSP_MODE_ETA && s->calg == ESPGPU_CRYPTO_AES_CBC;
-    if (have) {
-      const int pl = (int)len - 24 - (int)s->mlen;
-      have = pl > 0 && (pl & 15) == 0 && (len & 3) == 0;
-      len = have ? (uint32_t)pl : 0u;
-    }
-  }
-  uint64_t todo = __ballot(have);
-  while (todo) {
-    const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
-    const bool mine = have && sa == sau;
-    todo &= ~__ballot(mine);
-    have = have && !mine;
-    const DevSA *s = p.sas + sau;
-    const int nr = (int)s->nr;
-    if (!mine) continue;
-    uint8_t *rec = p.arena + off;
-    uint4 prev = ld16(rec + 8);
-    for (uint32_t i = 0; i < len / 16; ++i) {
-      prev = aes_enc(xor4(ld16(rec + 24 + 16 * i), prev), kp(s->rk), nr, lds, slot);
-      st16(rec + 24 + 16 * i, prev);
-    }
-  }
-}
-
-template <int WG>
-__global__ __launch_bounds__(WG, ETA_ENC2_WPE) void eta_cbc_enc2_kernel(EtaParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[65536];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t slot = (uint32_t)(lane & 31) * 4;
-  fill_pair(lds, LDS_T, p.tpair, tid, WG);
-  __syncthreads();
-  const uint32_t u0 = p.nchunks[0], nu = p.nchunks[1] - u0;
-  for (;;) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&p.queue[0], 2u);
-    t = __builtin_amdgcn_readfirstlane(t);
-    if (t >= nu) break;
-    uint32_t sa_a = 0, sa_b = 0;
-    bool mix_a = false, mix_b = false;
-    const CbcRec a = cbc_chunk_rec(p, u0 + t, lane, &sa_a, &mix_a);
-    const bool two = t + 1 < nu;
-    CbcRec b{nullptr, 0};
-    if (two) b = cbc_chunk_rec(p, u0 + t + 1, lane, &sa_b, &mix_b);
-    const int nra = sa_a < p.nsas ? (int)p.sas[sa_a].nr : 0, nrb = two && sa_b < p.nsas ? (int)p.sas[sa_b].nr : 0;
-    if (mix_a || mix_b || !two || nra != nrb) {       // wave-uniform
-      cbc_chunk_single(p, u0 + t, lane, lds, slot);
-      if (two) cbc_chunk_single(p, u0 + t + 1, lane, lds, slot);
-      continue;
-    }
-    const kptr ka = kp(p.sas[sa_a].rk), kb = kp(p.sas[sa_b].rk);
-    const uint32_t nmax = max(a.nb, b.nb);
-    uint4 pa = make_uint4(0, 0, 0, 0), pb = pa;
-    if (a.nb) pa = ld16(a.rec + 8);
-    if (b.nb) pb = ld16(b.rec + 8);
-    // ETA_ENC2_G blocks (16 G contiguous bytes) of each record per load and
-    // per store
-    constexpr int G = ETA_ENC2_G;
-    for (uint32_t i = 0; i < nmax; i += G) {
-      uint4 ma[G], mb[G];
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        ma[k] = i + k < a.nb ? ld16(a.rec + 24 + 16 * (i + k)) : make_uint4(0, 0, 0, 0);
-        mb[k] = i + k < b.nb ? ld16(b.rec + 24 + 16 * (i + k)) : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        if (i + k < nmax) {
-          uint4 x = xor4(ma[k], pa), y = xor4(mb[k], pb);
-          aes_enc_x2(x, y, ka, kb, nra, lds, slot);
-          if (i + k < a.nb) pa = ma[k] = x;
-          if (i + k < b.nb) pb = mb[k] = y;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        if (i + k < a.nb) st16(a.rec + 24 + 16 * (i + k), ma[k]);
-        if (i + k < b.nb) st16(b.rec + 24 + 16 * (i + k), mb[k]);
-      }
-    }
-  }
-  if (lane == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x * (WG / 64) - 1) {
-    atomicExch(&p.queue[0], 0u);
-    atomicExch(&p.queue[1], 0u);
-  }
-}
-
 }  // namespace
 
 int set_eta_opts(uint32_t opts) {
@@ -1928,9 +1735,7 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
   // sessions, bits 2/3 = SHA2-384/512 CBC / CTR sessions
   if (encrypt) {
     // cipher passes (lean, 1024 threads, up to 2 workgroups per CU), then the MAC pass
-    if ((kinds & 5) && ETA_ENC2 && p.chunks != nullptr)
-      hipLaunchKernelGGL((eta_cbc_enc2_kernel<1024>), dim3(2 * grid), dim3(1024), 0, st, p);
-    else if (kinds & 5)
+    if (kinds & 5)
       hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
     if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
     hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
