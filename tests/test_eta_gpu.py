@@ -108,6 +108,46 @@ def test_eta_encrypt_vs_oracle(drv):
         drv.freesession(s)
 
 
+@pytest.mark.parametrize("grouped", [False, True])
+def test_eta_encrypt_mixed_wave_vs_oracle(drv, grouped):
+    """Encrypt with every ETA transform mixed record by record (grouped: the
+    64-record units hold several sessions, so the cipher pass walks them one
+    session at a time and the quad-coalesced CBC chain and MAC pass run with
+    lanes switched off inside each quad), ragged payloads from one block to
+    jumbo, and records of no session among them (EINVAL, bytes untouched):
+    ciphertext and ICV bit-exact vs the oracle."""
+    from espgpu.batch import encrypt_batch
+    rng = np.random.default_rng(91 + grouped)
+    sas = [EtaSA(rng, 32), EtaSA(rng, 16, esn=True, sha=256), EtaSA(rng, 24, sha=384),
+           EtaSA(rng, 32, ctr=True, sha=1), EtaSA(rng, 16, noauth=True), EtaSA(rng, null=True, sha=256)]
+    sids = _sessions(drv, sas)
+    n = 1000
+    sa_idx = rng.integers(0, len(sas), n)
+    cts = _variant_cts(rng, sas, sa_idx)
+    plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts,
+                                         esn_hi=rng.integers(0, 2**32, n, dtype=np.uint32))
+    d = descs.copy()
+    d["sa"] = [sids[s] for s in sa_idx]
+    orphan = rng.random(n) < 0.05
+    d["sa"][orphan] = 0xFFFF                                  # no such session
+    arena = _dev(plain)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    encrypt_batch(drv, arena, _descs_dev(d), n, st, grouped=grouped)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert (st[orphan] == O.EINVAL).all() and (st[~orphan] == 0).all()
+    res = arena.cpu().numpy()
+    keep = np.zeros(len(plain), dtype=bool)
+    for i in range(n):
+        o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        keep[o:o + L] = True
+        want = plain[o:o + L] if orphan[i] else ct[o:o + L]
+        assert (res[o:o + L] == want).all(), (i, sa_idx[i], int(cts[i]), bool(orphan[i]))
+    assert (res[~keep] == plain[~keep]).all()                 # nothing outside the records
+    for s in sids:
+        drv.freesession(s)
+
+
 def test_mixed_gcm_and_eta_batch(drv):
     """One batch holding GCM and ETA records of several sessions (planner path)."""
     from espgpu.batch import decrypt_batch
