@@ -114,8 +114,9 @@ def test_eta_encrypt_mixed_wave_vs_oracle(drv, grouped):
     64-record units hold several sessions, so the cipher pass walks them one
     session at a time and the quad-coalesced CBC chain and MAC pass run with
     lanes switched off inside each quad), ragged payloads from one block to
-    jumbo, and records of no session among them (EINVAL, bytes untouched):
-    ciphertext and ICV bit-exact vs the oracle."""
+    jumbo, and records of no session or with a CBC payload that is not a
+    block multiple among them (EINVAL, bytes untouched): ciphertext and ICV
+    bit-exact vs the oracle."""
     from espgpu.batch import encrypt_batch
     rng = np.random.default_rng(91 + grouped)
     sas = [EtaSA(rng, 32), EtaSA(rng, 16, esn=True, sha=256), EtaSA(rng, 24, sha=384),
@@ -130,6 +131,11 @@ def test_eta_encrypt_mixed_wave_vs_oracle(drv, grouped):
     d["sa"] = [sids[s] for s in sa_idx]
     orphan = rng.random(n) < 0.05
     d["sa"][orphan] = 0xFFFF                                  # no such session
+    # CBC records whose payload is not a block multiple (xform_esp.c:316-324)
+    cbc = np.array([not (sas[i].ctr or sas[i].null) for i in sa_idx])
+    ragged = cbc & ~orphan & (rng.random(n) < 0.05)
+    d["len"][ragged] -= 4
+    orphan |= ragged
     arena = _dev(plain)
     st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
     encrypt_batch(drv, arena, _descs_dev(d), n, st, grouped=grouped)
@@ -141,7 +147,7 @@ def test_eta_encrypt_mixed_wave_vs_oracle(drv, grouped):
     for i in range(n):
         o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
         keep[o:o + L] = True
-        want = plain[o:o + L] if orphan[i] else ct[o:o + L]
+        want = plain[o:o + L] if orphan[i] else ct[o:o + L]   # refused records keep their bytes
         assert (res[o:o + L] == want).all(), (i, sa_idx[i], int(cts[i]), bool(orphan[i]))
     assert (res[~keep] == plain[~keep]).all()                 # nothing outside the records
     for s in sids:
