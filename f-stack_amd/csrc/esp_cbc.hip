@@ -62,6 +62,9 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_ENC_QUAD4
 #define ETA_ENC_QUAD4 1      // MODE 4 CBC: cbc_enc_quad (quad-coalesced 64-byte groups)
 #endif
+#ifndef ETA_WG1
+#define ETA_WG1 1024         // encrypt MAC pass (MODE 1) for SHA-1 / SHA2-256 / no-auth sessions
+#endif
 #ifndef ETA_STAGGER
 #define ETA_STAGGER 0        // probe: delay (s_memrealtime ticks) of the late-starting waves
 #endif
@@ -1308,7 +1311,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
         have = false;                                       // the fused launches' session
       } else if ((MODE == 5 || MODE == 6 || MODE == 8) && two_pass_only(s->calg, s->aalg)) {
         have = false;                                       // MODE 3's session
-      } else if ((MODE == 2 || MODE == 3 || MODE == 7) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
+      } else if ((MODE == 1 || MODE == 2 || MODE == 3 || MODE == 7) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
                                               (CKS == CK_WIDEH && !wide_hash(s->aalg)))) {
         have = false;                                       // the other hash set's launch
       } else {
@@ -1464,7 +1467,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
           for (uint32_t k = 0; k < s->mlen / 4; ++k)
             *reinterpret_cast<uint32_t *>(rec + hl + plen + 4 * k) = bswap32(dg[k]);
       }
-      if (have && valid && hq1 == 0 && p.sas[sa].aalg != 0) {   // CSP_MODE_CIPHER: no ICV
+      if (CKS != CK_NARROW && have && valid && hq1 == 0 && p.sas[sa].aalg != 0) {   // CSP_MODE_CIPHER: no ICV
         const DevSA *s = p.sas + sa;
         uint8_t *rec = p.arena + off;
         uint32_t dg[16];
@@ -1738,7 +1741,10 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     if (kinds & 5)
       hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
     if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
-    hipLaunchKernelGGL((eta_kernel<1, 768, -1>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    // MAC pass by hash width, as the in-place decrypt: SHA-1 / SHA2-256 / no
+    // auth without the SHA-512 code (1024 threads), SHA2-384/512 apart
+    hipLaunchKernelGGL((eta_kernel<1, ETA_WG1, CK_NARROW>), dim3(clamp(grid, ETA_WG1)), dim3(ETA_WG1), 0, st, p);
+    if (kinds & 16) hipLaunchKernelGGL((eta_kernel<1, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   } else if (fused) {
     // in place: the verify-first kernel (MODE 2); out of place: MODE 3 for
     // every session (eta_fused = 2, the default), or the one-pass MODE 0
