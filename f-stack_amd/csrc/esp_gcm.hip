@@ -85,6 +85,14 @@
 #ifndef GCM_RING
 #define GCM_RING 0
 #endif
+#ifndef GCM_H4_LDS
+#define GCM_H4_LDS 1  // session change: the 4-bit power table through LDS (stage_h8_lds)
+#endif
+#ifndef GCM_STAGE_INL
+// the table staging of a session change as a real call: kept out of the
+// record loop's register allocation (cfg1 in place: 16 -> 10 VGPRs spilled)
+#define GCM_STAGE_INL __noinline__
+#endif
 #ifndef GCM_XCDQ2
 #define GCM_XCDQ2 0  // per-XCD work-queue tickets (xcd_ticket) in gcm_kernel
 #endif
@@ -785,7 +793,7 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 // reference precomputes its tables once per key (gmac.c:48-63 -> gfmult.c:87
 // gf128_genmultable4); here the 8-bit expansion is redone per workgroup.
 template <int WG>
-__device__ __forceinline__ void stage_h8(uint8_t *dst, const uint8_t *t4, int tid) {
+__device__ GCM_STAGE_INL void stage_h8(uint8_t *dst, const uint8_t *t4, int tid) {
 #pragma unroll 1     // (unrolled, the allocator spills more in the record loop)
   for (int k = 0; k < (4096 + WG - 1) / WG; ++k) {
     const int e = tid + k * WG;
@@ -794,6 +802,44 @@ __device__ __forceinline__ void stage_h8(uint8_t *dst, const uint8_t *t4, int ti
       const uint4 lo = *reinterpret_cast<const uint4 *>(t4 + (2 * q) * 256 + (v & 15) * 16);
       const uint4 hi = *reinterpret_cast<const uint4 *>(t4 + (2 * q + 1) * 256 + (v >> 4) * 16);
       *reinterpret_cast<uint4 *>(dst + e * 16) = xor4(lo, hi);
+    }
+  }
+}
+
+// The Te0/Te1 pair table, 32 replicas, into LDS (a workgroup's first AEAD
+// chunk; out of line like the table staging)
+template <int WG>
+__device__ GCM_STAGE_INL void fill_tp(uint8_t *lds, const uint2 *tpair, int tid) {
+  for (int idx = tid; idx < 256 * 32; idx += WG) {
+    const int x = idx >> 5, r = idx & 31;
+    const uint2 t = tpair[x];
+    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
+    *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
+  }
+}
+
+// stage_h8 through LDS: the power's 8 KiB 4-bit table into `scratch` with
+// one coalesced 16-byte load per thread (one L2/HBM round trip instead of
+// stage_h8's four dependent ones per thread -- at a session change of every
+// chunk, as in cfg4, those round trips were the staging's cost), then the
+// 8-bit entries from LDS.  Entry slot e takes q = e & 15 and v = (e >> 4) +
+// 17q (mod 256), so a 16-lane group reads 16 different bank quads for the low
+// nibble's row, at most 2 lanes per quad for the high one, and writes 16
+// different quads.  Contains a barrier: call it workgroup-uniformly, after
+// the workgroup's last read of dst and scratch.
+template <int WG>
+__device__ GCM_STAGE_INL void stage_h8_lds(uint8_t *dst, const uint8_t *t4, int tid, uint8_t *scratch) {
+  for (int i = tid; i < (int)(kGhPowerBytes / 16); i += WG)
+    reinterpret_cast<uint4 *>(scratch)[i] = reinterpret_cast<const uint4 *>(t4)[i];
+  __syncthreads();
+#pragma unroll 1
+  for (int k = 0; k < (4096 + WG - 1) / WG; ++k) {
+    const int e = tid + k * WG;
+    if (4096 % WG == 0 || e < 4096) {
+      const int q = e & 15, v = ((e >> 4) + 17 * q) & 255;
+      const uint4 lo = *reinterpret_cast<const uint4 *>(scratch + (2 * q) * 256 + (v & 15) * 16);
+      const uint4 hi = *reinterpret_cast<const uint4 *>(scratch + (2 * q + 1) * 256 + (v >> 4) * 16);
+      *reinterpret_cast<uint4 *>(dst + (v * 16 + q) * 16) = xor4(lo, hi);
     }
   }
 }
@@ -1719,8 +1765,8 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   constexpr bool RING = GCM_RING && MODE == 0 && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
   constexpr bool FM = GCM_FMUL_LDS && !RING && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
   constexpr bool HB = GCM_HYBRID > 0 && !RING && !FM && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (RING ? kRingBytes : 0) + (FM ? kFmBytes : 0) +
-                                                      (HB ? kKpBytes : 0)];
+  constexpr uint32_t LDS_H4 = LDS_BYTES + (RING ? kRingBytes : 0) + (FM ? kFmBytes : 0) + (HB ? kKpBytes : 0);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_H4 + (GCM_H4_LDS ? kGhPowerBytes : 0)];
   const int tid = threadIdx.x;
   if (HB && GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(1);
   GCM_PHASE(0, true);
@@ -1775,17 +1821,16 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         mlen = s->mlen;
         mode = s->mode;
         if (mode == ESPGPU_CSP_MODE_AEAD && !tfilled) {
-          for (int idx = tid; idx < 256 * 32; idx += WG) {
-            const int x = idx >> 5, r = idx & 31;
-            const uint2 t = p.tpair[x];
-            *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + r * 4) = t.x;
-            *reinterpret_cast<uint32_t *>(lds + LDS_TP + x * 256 + 128 + r * 4) = t.y;
-          }
+          fill_tp<WG>(lds, p.tpair, tid);
           tfilled = true;
           GCM_PHASE(1, true);
         }
         if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
-          stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
+          if (GCM_H4_LDS)
+            stage_h8_lds<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes,
+                             tid, lds + LDS_H4);
+          else
+            stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
           if (HB && nr == 10) stage_kp<WG>(lds + LDS_KP, (rkptr)(const void *)(p.sas[sa].dk), tid);
           if (FM && !implicit) {
             // H^1..H^3 (power index i = 0..2): position-major in gtab (j*256 +
@@ -1903,8 +1948,13 @@ __device__ __forceinline__ void burst_chunk(const GcmParams &p, uint8_t *lds, ui
       ss.flags = s->flags;
       ss.mlen = s->mlen;
       ss.mode = s->mode;
-      if (ss.mode == ESPGPU_CSP_MODE_AEAD)    // H^8 (power index 7)
-        stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid);
+      if (ss.mode == ESPGPU_CSP_MODE_AEAD) {  // H^8 (power index 7)
+        if (GCM_H4_LDS)
+          stage_h8_lds<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid,
+                           lds + LDS_BYTES);
+        else
+          stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid);
+      }
     } else {
       ss.mode = 0;
     }
@@ -2014,7 +2064,7 @@ template <int DIR, int WG, bool STAGE = false>
 __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
   [[maybe_unused]] constexpr int S = kGcmLanesSmall;    // for the phase clock
   GCM_PHASE(0, true);
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (GCM_H4_LDS ? kGhPowerBytes : 0)];
   const int tid = threadIdx.x;
   load_tpair<WG>(lds, p.tpair);
   GCM_PHASE(1, true);
@@ -2059,7 +2109,7 @@ __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
 // claim (poll() relaunches the kernel for a job published after that).
 template <int WG>
 __global__ __launch_bounds__(WG) void gcm_door_kernel(DoorArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (GCM_H4_LDS ? kGhPowerBytes : 0)];
   __shared__ uint4 s_z[kChunkRecs];
   __shared__ XferSpan s_xout[2 * kChunkRecs];
   __shared__ uint32_t s_cmd[2][4];                 // job, chunk, n, slot_op (double-buffered by parity)
