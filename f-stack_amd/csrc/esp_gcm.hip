@@ -844,6 +844,36 @@ __device__ GCM_STAGE_INL void stage_h8_lds(uint8_t *dst, const uint8_t *t4, int 
   }
 }
 
+// In place, one pass (MODE 3, GCM_INPLACE_ONEPASS): a record whose tag
+// failed already holds plaintext; XORing the same keystream over it again
+// restores the ciphertext exactly, so the buffer ends as cryptosoft's
+// verify-first leaves it (cryptosoft.c:595-633: a failed record is not
+// decrypted).  Rare path, one block per lane per step, with its own counter
+// cache: it runs only in a wave with a failed record, after the wave's stores
+// are complete (the block-to-lane map here differs from the GHASH
+// schedule's), and out of line, so the record loop does not hold registers
+// for it.  Every lane of the wave calls it (back: this lane's record).
+template <int S>
+__device__ GCM_STAGE_INL void gcm_rollback(uint8_t *rec, int nct, int ct_len, bool back, int l, uint32_t s0c,
+                                          uint32_t s1c, uint32_t s2c, rkptr rk, uint32_t rk3, int nr,
+                                          const uint8_t *lds, uint32_t slot) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  CtrCache cc;
+  cc.hi = -1;
+  int Mr = back ? (nct + S - 1) / S : 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
+  for (int a = 0; a < Mr; ++a) {
+    const int c = S * a + l;
+    const uint32_t t = (uint32_t)c + 2;
+    uint4 P = make_uint4(0, 0, 0, 0);
+    if (back && c < nct) P = ld16(rec + 16 + 16 * c);
+    if ((int)(t >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(t >> 8), rk, lds, slot);
+    const uint4 ks = aes_ctr(cc, t, rk3, nr, rk, lds, slot);
+    if (back && c < nct) st_partial(rec + 16 + 16 * c, xor4(P, ks), ct_len - 16 * c);
+  }
+}
+
 // ---- one 8-record group per wave -----------------------------------------------
 // MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
 // MODE 1: encrypt in place + ICV
@@ -1299,29 +1329,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       ok = ((d.x | d.y | d.z | d.w) == 0);
     }
   }
-  if (MODE == 3 && __any(valid && !ok)) {
-    // In place, one pass (MODE 3, GCM_INPLACE_ONEPASS): a record whose tag
-    // failed already holds plaintext; XORing the same keystream over it again
-    // restores the ciphertext exactly, so the buffer ends as cryptosoft's
-    // verify-first leaves it (cryptosoft.c:595-633: a failed record is not
-    // decrypted).  Rare path, one block per lane per step (small code): it
-    // runs only in a wave with a failed record, after the wave's stores are
-    // complete (the block-to-lane map here differs from the GHASH schedule's).
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    const int back = valid && !ok;
-    int Mr = back ? (nct + S - 1) / S : 0;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
-    for (int a = 0; a < Mr; ++a) {
-      const int c = S * a + l;
-      const uint32_t t = (uint32_t)c + 2;
-      uint4 P = make_uint4(0, 0, 0, 0);
-      if (back && c < nct) P = ld16(rec + 16 + 16 * c);
-      if ((int)(t >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(t >> 8), rk, lds, slot);
-      const uint4 ks = aes_ctr(cc, t, rk3, nr, rk, lds, slot);
-      if (back && c < nct) st_partial(rec + 16 + 16 * c, xor4(P, ks), ct_len - 16 * c);
-    }
-  }
+  if (MODE == 3 && __any(valid && !ok))
+    gcm_rollback<S>(rec, nct, ct_len, valid && !ok, l, s0c, s1c, s2c, rk, rk3, nr, lds, slot);
   if (MODE == 2) {
     // pass 2: CTR decrypt in place, only for authenticated records.  No GHASH
     // here, so the CT blocks are dealt densely (lane l of step a: block
