@@ -89,8 +89,10 @@
 #define GCM_H4_LDS 1  // session change: the 4-bit power table through LDS (stage_h8_lds)
 #endif
 #ifndef GCM_STAGE_INL
-// the table staging of a session change as a real call: kept out of the
-// record loop's register allocation (cfg1 in place: 16 -> 10 VGPRs spilled)
+// the cold work of the chunk loop (session-change table staging, the first
+// T-table fill, MODE 3's rollback of a failed record) as real calls: kept
+// out of the record loop's register allocation (gcm_kernel<3,1024,4>: 16 ->
+// 0 VGPRs spilled)
 #define GCM_STAGE_INL __noinline__
 #endif
 #ifndef GCM_XCDQ2
