@@ -86,7 +86,10 @@ __global__ __launch_bounds__(PWG) void plan_scan(uint32_t *gcnt, uint32_t nsas, 
   const uint32_t per = (nkeys + PWG - 1) / PWG;
   const uint32_t k0 = threadIdx.x * per, k1 = min(nkeys, k0 + per);
   const uint32_t eta0 = 4 * nsas + 1;                       // first ETA key
-  auto recs_per_chunk = [&](uint32_t k) { return k >= eta0 ? 64u : (uint32_t)kChunkRecs; };
+  static_assert(kChunkRecs == 256, "chunks_of: 256-record GCM chunks");
+  // chunks of key k: 64-record ETA chunks, 256-record GCM / invalid ones
+  // (shifts: a run-time divisor was a full integer division per key)
+  auto chunks_of = [&](uint32_t k, uint32_t cnt) { return k >= eta0 ? (cnt + 63u) >> 6 : (cnt + 255u) >> 8; };
   // The counts into LDS with coalesced, independent loads (a thread's run of
   // keys read from global memory one dependent load after another was most
   // of this kernel's time), then zeroed for the next plan: each thread clears
@@ -99,20 +102,39 @@ __global__ __launch_bounds__(PWG) void plan_scan(uint32_t *gcnt, uint32_t nsas, 
   for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t cnt = s_cnt[k];
     r += cnt;
-    c += (cnt + recs_per_chunk(k) - 1) / recs_per_chunk(k);
+    c += chunks_of(k, cnt);
   }
-  s_rec[threadIdx.x] = r;
-  s_chk[threadIdx.x] = c;
+  // inclusive scan of the 1024 partials: within each wave by shuffles, then
+  // over the 16 wave totals (3 barriers instead of Hillis-Steele's 20)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t ri = r, ci = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t a = __shfl_up(ri, o), b = __shfl_up(ci, o);
+    if (lane >= o) {
+      ri += a;
+      ci += b;
+    }
+  }
+  if (lane == 63) {
+    s_rec[wave] = ri;
+    s_chk[wave] = ci;
+  }
   __syncthreads();
-  for (int o = 1; o < PWG; o <<= 1) {
-    uint32_t a = threadIdx.x >= (unsigned)o ? s_rec[threadIdx.x - o] : 0;
-    uint32_t b = threadIdx.x >= (unsigned)o ? s_chk[threadIdx.x - o] : 0;
-    __syncthreads();
-    s_rec[threadIdx.x] += a;
-    s_chk[threadIdx.x] += b;
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t ar = 0, ac = 0;
+    for (int w = 0; w < PWG / 64; ++w) {
+      const uint32_t tr = s_rec[w], tc = s_chk[w];
+      s_rec[w] = ar;                       // exclusive wave offsets
+      s_chk[w] = ac;
+      ar += tr;
+      ac += tc;
+    }
+    s_rec[PWG / 64] = ar;                  // the totals
+    s_chk[PWG / 64] = ac;
   }
-  uint32_t roff = s_rec[threadIdx.x] - r, coff = s_chk[threadIdx.x] - c;
+  __syncthreads();
+  uint32_t roff = s_rec[wave] + ri - r, coff = s_chk[wave] + ci - c;
   for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t cnt = s_cnt[k];
     gcur[k] = roff;                       // record cursor (plan_scatter) = the key's first record
@@ -121,11 +143,11 @@ __global__ __launch_bounds__(PWG) void plan_scan(uint32_t *gcnt, uint32_t nsas, 
     // the GCM kernel's share: the chunks before the first ETA key
     if (k == eta0) nchunks[0] = min(coff, max_chunks);
     roff += cnt;
-    coff += (cnt + recs_per_chunk(k) - 1) / recs_per_chunk(k);
+    coff += chunks_of(k, cnt);
   }
   if (threadIdx.x == PWG - 1) {
-    const uint32_t total = s_chk[PWG - 1];
-    groff[nkeys] = s_rec[PWG - 1];
+    const uint32_t total = s_chk[PWG / 64];
+    groff[nkeys] = s_rec[PWG / 64];
     gcoff[nkeys] = total;
     nchunks[1] = min(total, max_chunks);
     if (eta0 >= nkeys) nchunks[0] = min(total, max_chunks);   // no ETA keys (no sessions)
