@@ -65,6 +65,12 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_WG1
 #define ETA_WG1 1024         // encrypt MAC pass (MODE 1) for SHA-1 / SHA2-256 / no-auth sessions
 #endif
+#ifndef ETA_HQ_NB1
+#define ETA_HQ_NB1 2         // MAC pass (MODE 1): hmac_quad blocks per load
+#endif
+#ifndef ETA_HQ_NB2
+#define ETA_HQ_NB2 2         // in-place verify (MODE 2): hmac_quad blocks per load
+#endif
 #ifndef ETA_STAGGER
 #define ETA_STAGGER 0        // probe: delay (s_memrealtime ticks) of the late-starting waves
 #endif
@@ -594,7 +600,10 @@ __device__ __forceinline__ void quad_transpose4(uint32_t (&A)[4], bool qb0, bool
   }
 }
 
-template <int HS>
+// NB = 2: each iteration loads blocks b and b + 1 together (a record's 128
+// contiguous bytes at once, so the line they share is fetched once), then
+// compresses them one after the other.
+template <int HS, int NB = 1>
 __device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi, kptr ipad,
                           kptr opad, uint32_t out[8]) {
   constexpr int W = Hash<HS>::W;
@@ -619,10 +628,18 @@ __device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, u
   uint32_t tw = total;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) tw = max(tw, (uint32_t)__shfl_xor((int)tw, o));
-  for (uint32_t b = 0; b <= tw; ++b) {            // wave-uniform trip count
-    uint4 P[4];
+  for (uint32_t b0 = 0; b0 <= tw; b0 += NB) {     // wave-uniform trip count
+  uint4 PP[NB][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) P[i] = b < pn[i] ? ld16(pr[i] + 64 * b + 16 * q) : make_uint4(0, 0, 0, 0);
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      PP[nb][i] = b0 + nb < pn[i] ? ld16(pr[i] + 64 * (b0 + nb) + 16 * q) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const uint32_t b = b0 + nb;
+    if (nb > 0 && b > tw) continue;               // (wave-uniform)
+    const uint4 *P = PP[nb];
     uint32_t X[4] = {P[0].x, P[1].x, P[2].x, P[3].x}, Y[4] = {P[0].y, P[1].y, P[2].y, P[3].y};
     uint32_t Z[4] = {P[0].z, P[1].z, P[2].z, P[3].z}, V[4] = {P[0].w, P[1].w, P[2].w, P[3].w};
     quad_transpose4(X, qb0, qb1);
@@ -656,6 +673,7 @@ __device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, u
         Hash<HS>::compress(h, w);
       }
     }
+  }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) out[k] = h[k];
@@ -1365,9 +1383,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
         const uint8_t *rec = p.arena + off;
         uint32_t dg[16];
         if (hs == 2)
-          hmac_quad<HS_SHA256>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
+          hmac_quad<HS_SHA256, ETA_HQ_NB2>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
         else
-          hmac_quad<HS_SHA1>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
+          hmac_quad<HS_SHA1, ETA_HQ_NB2>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
         if (act) {
           uint32_t diff = 0;
           for (uint32_t k = 0; k < hq_mlen / 4; ++k)
@@ -1458,11 +1476,11 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
         uint8_t *rec = p.arena + off;
         uint32_t dg[16];
         if (hs == 2)
-          hmac_quad<HS_SHA256>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
-                               kp(s->opad), dg);
+          hmac_quad<HS_SHA256, ETA_HQ_NB1>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh,
+                                           kp(s->ipad), kp(s->opad), dg);
         else
-          hmac_quad<HS_SHA1>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
-                             kp(s->opad), dg);
+          hmac_quad<HS_SHA1, ETA_HQ_NB1>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh,
+                                         kp(s->ipad), kp(s->opad), dg);
         if (act)
           for (uint32_t k = 0; k < s->mlen / 4; ++k)
             *reinterpret_cast<uint32_t *>(rec + hl + plen + 4 * k) = bswap32(dg[k]);
