@@ -71,6 +71,12 @@ constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode =
 #ifndef ETA_HQ_NB2
 #define ETA_HQ_NB2 2         // in-place verify (MODE 2): hmac_quad blocks per load
 #endif
+#ifndef ETA_ENC_NB
+#define ETA_ENC_NB 1         // cbc_enc_quad: 64-byte groups per load / store
+#endif
+#ifndef ETA_ENC_WPE
+#define ETA_ENC_WPE 8        // MODE 4 CBC: minimum waves per SIMD (8: <= 64 VGPRs, two workgroups per CU)
+#endif
 #ifndef ETA_STAGGER
 #define ETA_STAGGER 0        // probe: delay (s_memrealtime ticks) of the late-starting waves
 #endif
@@ -687,6 +693,7 @@ __device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, u
 // contiguous bytes instead of 64 records x 16 bytes.  Every lane of the wave
 // calls it (act = this lane's record is encrypted); the loop runs to the
 // wave's longest record.  ek: the wave-uniform encryption schedule.
+template <int NB>
 __device__ void cbc_enc_quad(bool act, uint8_t *rec, uint32_t nb0, kptr ek, int nr, const uint8_t *lds,
                              uint32_t slot) {
   const int lane = threadIdx.x & 63, q = lane & 3;
@@ -703,52 +710,76 @@ __device__ void cbc_enc_quad(bool act, uint8_t *rec, uint32_t nb0, kptr ek, int 
     return (uint8_t *)(uintptr_t)(((uint64_t)qbcast<i>(rhi) << 32) | qbcast<i>(rlo));
   };
   auto pn = [&](auto I) { return qbcast<decltype(I)::value>(nb); };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
   uint32_t nw = nb;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) nw = max(nw, (uint32_t)__shfl_xor((int)nw, o));
   nw = __builtin_amdgcn_readfirstlane(nw);        // (equal on every lane: a scalar loop)
   uint4 prev = act ? ld16(rec + 8) : make_uint4(0, 0, 0, 0);   // IV
-  for (uint32_t b = 0; b < nw; b += 4) {          // wave-uniform trip count
-    uint4 P[4];
-    auto ld = [&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const uint8_t *a = pr(I);                    // (DPP: every lane, outside the branch)
-      P[i] = b + q < pn(I) ? ld16(a + 24 + 16 * (b + q)) : make_uint4(0, 0, 0, 0);
-    };
-    ld(std::integral_constant<int, 0>{});
-    ld(std::integral_constant<int, 1>{});
-    ld(std::integral_constant<int, 2>{});
-    ld(std::integral_constant<int, 3>{});
-    uint32_t X[4] = {P[0].x, P[1].x, P[2].x, P[3].x}, Y[4] = {P[0].y, P[1].y, P[2].y, P[3].y};
-    uint32_t Z[4] = {P[0].z, P[1].z, P[2].z, P[3].z}, V[4] = {P[0].w, P[1].w, P[2].w, P[3].w};
-    quad_transpose4(X, qb0, qb1);
-    quad_transpose4(Y, qb0, qb1);
-    quad_transpose4(Z, qb0, qb1);
-    quad_transpose4(V, qb0, qb1);
+  // NB 64-byte groups (4 blocks each) per iteration: loaded together, chained,
+  // stored together (NB = 2: a record's 128 contiguous bytes move at once)
+  for (uint32_t b0 = 0; b0 < nw; b0 += 4 * NB) {  // wave-uniform trip count
+    uint32_t X[NB][4], Y[NB][4], Z[NB][4], V[NB][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {                 // block b + k of this lane's record
-      if (b + k < nb) {
-        prev = aes_enc(xor4(make_uint4(X[k], Y[k], Z[k], V[k]), prev), ek, nr, lds, slot);
-        X[k] = prev.x;
-        Y[k] = prev.y;
-        Z[k] = prev.z;
-        V[k] = prev.w;
+    for (int g = 0; g < NB; ++g) {
+      const uint32_t b = b0 + 4 * g;
+      uint4 P[4];
+      auto ld = [&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint8_t *a = pr(I);                  // (DPP: every lane, outside the branch)
+        P[i] = b + q < pn(I) ? ld16(a + 24 + 16 * (b + q)) : make_uint4(0, 0, 0, 0);
+      };
+      ld(I0{});
+      ld(I1{});
+      ld(I2{});
+      ld(I3{});
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        X[g][i] = P[i].x;
+        Y[g][i] = P[i].y;
+        Z[g][i] = P[i].z;
+        V[g][i] = P[i].w;
       }
     }
-    quad_transpose4(X, qb0, qb1);                 // (its own inverse)
-    quad_transpose4(Y, qb0, qb1);
-    quad_transpose4(Z, qb0, qb1);
-    quad_transpose4(V, qb0, qb1);
-    auto st = [&](auto I) {
-      constexpr int i = decltype(I)::value;
-      uint8_t *a = pr(I);                          // (DPP: every lane, outside the branch)
-      const bool in = b + q < pn(I);
-      if (in) st16(a + 24 + 16 * (b + q), make_uint4(X[i], Y[i], Z[i], V[i]));
-    };
-    st(std::integral_constant<int, 0>{});
-    st(std::integral_constant<int, 1>{});
-    st(std::integral_constant<int, 2>{});
-    st(std::integral_constant<int, 3>{});
+#pragma unroll
+    for (int g = 0; g < NB; ++g) {
+      const uint32_t b = b0 + 4 * g;
+      quad_transpose4(X[g], qb0, qb1);
+      quad_transpose4(Y[g], qb0, qb1);
+      quad_transpose4(Z[g], qb0, qb1);
+      quad_transpose4(V[g], qb0, qb1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {               // block b + k of this lane's record
+        if (b + k < nb) {
+          prev = aes_enc(xor4(make_uint4(X[g][k], Y[g][k], Z[g][k], V[g][k]), prev), ek, nr, lds, slot);
+          X[g][k] = prev.x;
+          Y[g][k] = prev.y;
+          Z[g][k] = prev.z;
+          V[g][k] = prev.w;
+        }
+      }
+      quad_transpose4(X[g], qb0, qb1);            // (its own inverse)
+      quad_transpose4(Y[g], qb0, qb1);
+      quad_transpose4(Z[g], qb0, qb1);
+      quad_transpose4(V[g], qb0, qb1);
+    }
+#pragma unroll
+    for (int g = 0; g < NB; ++g) {
+      const uint32_t b = b0 + 4 * g;
+      auto st = [&](auto I) {
+        constexpr int i = decltype(I)::value;
+        uint8_t *a = pr(I);                        // (DPP: every lane, outside the branch)
+        const bool in = b + q < pn(I);
+        if (in) st16(a + 24 + 16 * (b + q), make_uint4(X[g][i], Y[g][i], Z[g][i], V[g][i]));
+      };
+      st(I0{});
+      st(I1{});
+      st(I2{});
+      st(I3{});
+    }
   }
 }
 
@@ -1249,7 +1280,7 @@ __device__ __forceinline__ bool eta_interleaved(const EtaParams &p, const uint8_
 #define ETA_C8_WG 512
 #endif
 template <int MODE, int WG, int CKS>
-__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8 : 1) void eta_kernel(EtaParams p) {
+__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? ETA_ENC_WPE : 1) void eta_kernel(EtaParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
@@ -1375,8 +1406,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
     }
     if (ETA_HMAC_QUAD && MODE == 2 && CKS == CK_NARROW) {
       // the verify of this unit's records, the whole wave at once
-#pragma unroll
-      for (int hs = 1; hs <= 2; ++hs) {
+      for (int hs = 1; hs <= 2; ++hs) {           // (not unrolled: two hmac_quad bodies)
         if (!__any(hq == hs)) continue;           // wave-uniform
         const bool act = hq == hs;
         const DevSA *s = p.sas + (act ? sa : 0u);
@@ -1414,7 +1444,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
         const DevSA *s = p.sas + sau;
         const int nr = (int)s->nr;
         if (CKS == CK_CBC && ETA_ENC_QUAD4) {       // (the whole wave)
-          cbc_enc_quad(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
+          cbc_enc_quad<ETA_ENC_NB>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
           continue;
         }
         if (!mine) continue;
@@ -1468,8 +1498,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? 8
         const uint32_t aa = p.sas[sa].aalg;
         hq1 = aa == ESPGPU_CRYPTO_SHA1_HMAC ? 1 : aa == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 0;
       }
-#pragma unroll
-      for (int hs = 1; hs <= 2; ++hs) {
+      for (int hs = 1; hs <= 2; ++hs) {           // (not unrolled: two hmac_quad bodies)
         if (!ETA_ENC_QUAD || !__any(hq1 == hs)) continue;     // wave-uniform
         const bool act = hq1 == hs;
         const DevSA *s = p.sas + (act ? sa : 0u);
