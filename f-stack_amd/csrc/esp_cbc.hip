@@ -18,7 +18,10 @@
 //  * HMAC is a serial chain per record, so lane = record: each lane runs its
 //    record's SHA-1 / SHA-256 compressions from the precomputed ipad/opad
 //    chaining states (hmac_init_pad, crypto.c:413-441), rounds fully
-//    unrolled in registers, no tables.
+//    unrolled in registers, no tables.  The in-place verify and the MAC pass
+//    move the bytes through the quad (hmac_quad: lane 4Q+k loads piece k of
+//    the quad's four records, a DPP transpose hands each lane its own), two
+//    64-byte blocks per load.
 //  * Decrypt is verify-first: an HMAC pass (lane = record), then a
 //    block-parallel decrypt of the verified records (MODE 3 out of place, the
 //    default and benchmarked path; MODE 2 in place).  MODE 0 (set_tuning
@@ -33,8 +36,9 @@
 //  * AES uses T-table pairs replicated 32x in LDS (conflict-free ds_read_b32,
 //    one v_perm_b32 per address, as in esp_gcm.hip): Td0/Td1 + a replicated
 //    inverse S-box for CBC decryption, Te0/Te1 for CBC encryption and CTR.
-//  * CBC encryption is serial per record (lane = record); CTR encryption runs
-//    the same lane = record loop with independent blocks.
+//  * CBC encryption is serial per record (lane = record; its 64-byte groups
+//    moved through the quad as the hash blocks, cbc_enc_quad); CTR encryption
+//    runs the same lane = record loop with independent blocks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
