@@ -95,6 +95,9 @@
 // 0 VGPRs spilled)
 #define GCM_STAGE_INL __noinline__
 #endif
+#ifndef GCM_FMU
+#define GCM_FMU 1     // throughput kernel's final multiply: words per L2 round trip (1, 2 or 4)
+#endif
 #ifndef GCM_XCDQ2
 #define GCM_XCDQ2 0  // per-XCD work-queue tickets (xcd_ticket) in gcm_kernel
 #endif
@@ -751,11 +754,11 @@ __device__ __forceinline__ uint4 gf_mul4_lds(uint4 x, const uint8_t *lds, uint32
 // table addresses stay one pointer instead of 16 hoisted 64-bit ones (the
 // throughput kernels); unrolled, all 32 gathers are in flight at once instead
 // of four dependent L2 round trips (the small-batch kernels' latency).
-template <bool ROLLED = true>
+template <int UNR = 1>
 __device__ __forceinline__ uint4 gf_mul4_global(uint4 x, const uint8_t *t) {
   uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
   uint32_t w = x.x, w1 = x.y, w2 = x.z, w3 = x.w;
-  constexpr int kUnroll = ROLLED ? 1 : 4;
+  constexpr int kUnroll = UNR;
 #pragma unroll kUnroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t hi = w & 0xF0F0F0F0u, lo = (w << 4) & 0xF0F0F0F0u;
@@ -1315,7 +1318,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   else if (FM && fm)
     Z = l == 0 ? gf_mul8(Y, lds, gl) : gf_mul4_lds(Y, lds, LDS_FM + (uint32_t)(S - 1 - l) * kGhPowerBytes, lane);
   else
-    Z = gf_mul4_global<true>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+    Z = gf_mul4_global<GCM_FMU>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 ej0 = shfl4(EJ0, (lane & ~(S - 1)) | pad);
@@ -1571,7 +1574,7 @@ __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds
   }
   GCM_PHASE_T(10, true, kBurstCtrWaves * 64);
   if (zs != nullptr) {
-    uint4 Z = gf_mul4_global<S != kGcmLanesSmall>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+    uint4 Z = gf_mul4_global<S != kGcmLanesSmall ? 1 : 4>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
     for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
     if (have && l == 0) zs[zi] = Z;
@@ -1592,7 +1595,7 @@ __device__ __forceinline__ void tag_group(const GcmParams &p, const uint8_t *lds
       }
     }
   }
-  uint4 Z = gf_mul4_global<S != kGcmLanesSmall>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+  uint4 Z = gf_mul4_global<S != kGcmLanesSmall ? 1 : 4>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 T = xor4(Z, ej0);
