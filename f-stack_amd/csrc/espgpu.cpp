@@ -10,6 +10,7 @@
 //   process       cryptosoft.c:1429-1441 (swcr_process) -> swcr_gcm :465 / swcr_eta :874
 //   completion    crypto_done, crypto.c:1802
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +24,7 @@
 
 #include "espgpu.h"
 #include "espgpu_internal.h"
+#include "fifo_arena.h"
 #include "host_crypto.h"
 
 using namespace espgpu;
@@ -75,45 +77,9 @@ struct OvfEntry {
   int32_t sid;
   uint8_t op, kind;
 };
-// A fixed-capacity FIFO of variable-length contiguous allocations (a bip
-// buffer): allocated in arrival order, freed oldest first, wrapping to the
-// start when the end has no room.  Allocated once; never grows or moves, so
-// process() never reallocates or copies it.
-template <class T>
-struct FifoArena {
-  std::unique_ptr<T[]> buf;
-  size_t cap = 0, head = 0, tail = 0;
-  bool wrapped = false;              // the newest allocations sit in [0, tail) below head
-  void init(size_t n) {
-    buf.reset(n ? new T[n] : nullptr);
-    cap = n;
-    clear();
-  }
-  void clear() { head = tail = 0; wrapped = false; }
-  struct Mark { size_t head, tail; bool wrapped; };
-  Mark mark() const { return {head, tail, wrapped}; }
-  void undo(const Mark &m) { head = m.head; tail = m.tail; wrapped = m.wrapped; }
-  // offset of n contiguous elements, or SIZE_MAX when there is no room
-  size_t alloc(size_t n) {
-    if (n == 0) return 0;
-    if (!wrapped) {
-      if (tail + n <= cap) { tail += n; return tail - n; }
-      if (n <= head) { wrapped = true; tail = n; return 0; }
-      return SIZE_MAX;
-    }
-    if (tail + n <= head) { tail += n; return tail - n; }
-    return SIZE_MAX;
-  }
-  // free the oldest allocation [off, off + n)
-  void pop(size_t off, size_t n) {
-    if (n == 0) return;
-    if (wrapped && off < head) wrapped = false;    // the first allocation after the wrap
-    head = off + n;
-  }
-};
-
 // The host overflow: entries in a fixed ring, their gathered bytes and segment
-// lists in fixed FIFO arenas, all sized at set_tuning("overflow_mb").
+// lists in fixed FIFO arenas (fifo_arena.h), all sized at
+// set_tuning("overflow_mb").
 struct Overflow {
   std::unique_ptr<OvfEntry[]> ent;
   size_t ecap = 0, head = 0, count = 0;   // ring of entries; head = oldest
@@ -122,15 +88,24 @@ struct Overflow {
   size_t live_bytes = 0, peak_bytes = 0;
   bool empty() const { return count == 0; }
   OvfEntry &front() { return ent[head]; }
-  void init(size_t cap_bytes) {
+  // Reserve the three rings (the overflow must be empty).  All or nothing:
+  // false leaves the old rings in place (the caller answers ENOMEM; no
+  // exception crosses the C ABI).
+  bool init(size_t cap_bytes) {
     // the byte ring holds overflow_mb of records; entries (a zero-copy record
     // needs no bytes) and segment lists get rings of their own beside it
-    ecap = cap_bytes ? std::max<size_t>(256, std::min<size_t>(cap_bytes / 512, (size_t)1 << 22)) : 0;
-    ent.reset(ecap ? new OvfEntry[ecap] : nullptr);
-    bytes.init(cap_bytes);
-    segpool.init(ecap * 4);
+    const size_t ne = cap_bytes ? std::max<size_t>(256, std::min<size_t>(cap_bytes / 512, (size_t)1 << 22)) : 0;
+    std::unique_ptr<OvfEntry[]> e(ne ? new (std::nothrow) OvfEntry[ne] : nullptr);
+    FifoArena<uint8_t> b;
+    FifoArena<espgpu_seg> sg;
+    if ((ne && !e) || !b.init(cap_bytes) || !sg.init(ne * 4)) return false;
+    ent.swap(e);
+    ecap = ne;
+    bytes.swap(b);
+    segpool.swap(sg);
     head = count = 0;
     live_bytes = peak_bytes = 0;
+    return true;
   }
   size_t reserved() const {
     return ecap * sizeof(OvfEntry) + bytes.cap + segpool.cap * sizeof(espgpu_seg);
@@ -191,6 +166,9 @@ struct Slot {
   int64_t door_job = -1;
   uint64_t door_t0 = 0;
   uint4 *d_ej0 = nullptr;
+  uint64_t t_launch = 0;                    // host clock (ns) when the batch was launched / published
+  bool stuck = false;                       // fault injection: its completion is never seen (set_tuning "fault" 4)
+  hipStream_t wq = nullptr;                 // launch in progress: the stream host-writing work went to
 };
 
 }  // namespace
@@ -282,6 +260,11 @@ struct espgpu_ctx {
   hipStream_t last_st = nullptr;
   bool launched = false;
   hipEvent_t ev_last = nullptr;
+  // GPU failure (ctx_fail): once set the ctx launches nothing again; every
+  // request it holds completes exactly once with ESPGPU_EIO
+  bool failed = false;
+  uint32_t fault = 0;            // set_tuning "fault": injected failures (ESPGPU_FAULT_*)
+  uint32_t deadline_ms = 2000;   // set_tuning "deadline_ms": a batch outstanding this long is a GPU failure
   espgpu_stats stats{};
   float last_ms = 0.f;
   std::string err;
@@ -475,15 +458,18 @@ int door_write_slot(espgpu_ctx *c, size_t k) {
 // The kernel has exited (or was never launched): no workgroup reads the
 // slot table or the SA table's cached state any more.
 bool door_exited(espgpu_ctx *c) {
-  if (c->door_live && hipEventQuery(c->ev_door) == hipSuccess) c->door_live = false;
+  // (an error other than "not ready": the device is gone, and so is the kernel)
+  if (c->door_live && hipEventQuery(c->ev_door) != hipErrorNotReady) c->door_live = false;
   return !c->door_live;
 }
 
 // Stop the persistent kernel and wait for it (published jobs it did not
-// claim stay in the ring for the next launch).
+// claim stay in the ring for the next launch).  A failed ctx only asks: its
+// kernel may never finish, and nothing waits on a failed device.
 void door_stop(espgpu_ctx *c) {
   if (!c->door_live) return;
   __atomic_store_n(&c->door_ctl->stop, kDoorStopNow, __ATOMIC_SEQ_CST);
+  if (c->failed) return;
   hipEventSynchronize(c->ev_door);
   __atomic_store_n(&c->door_ctl->stop, 0u, __ATOMIC_SEQ_CST);
   c->door_live = false;
@@ -502,6 +488,17 @@ void door_retire(espgpu_ctx *c) {
   if (door_exited(c)) return;
   __atomic_store_n(&c->door_ctl->stop, kDoorStopIdle, __ATOMIC_SEQ_CST);
   c->door_retiring = true;
+}
+
+// No launched work of the ctx is outstanding: its last launch (any stream)
+// and every launched slot's batch have completed.  Until then a retire
+// request must stand: the launched work may sit behind the door kernel on a
+// shared hardware queue.
+bool launched_idle(espgpu_ctx *c) {
+  if (c->launched && hipEventQuery(c->ev_last) != hipSuccess) return false;
+  for (const Slot &s : c->slots)
+    if (s.state == SLOT_INFLIGHT && s.door_job < 0 && hipEventQuery(s.done) != hipSuccess) return false;
+  return true;
 }
 
 int door_launch(espgpu_ctx *c) {
@@ -578,6 +575,108 @@ bool door_done(const espgpu_ctx *c, int64_t job) {
   return __atomic_load_n(&c->door_ctl->done[j % kDoorRing], __ATOMIC_ACQUIRE) == j + 1;
 }
 
+// ---- GPU failure --------------------------------------------
+// A launch or copy that cannot be queued, a completion query that returns an
+// error, or a batch outstanding for deadline_ms is a GPU failure.  The ctx
+// then launches nothing again, and every request it holds completes exactly
+// once (crypto_done once per cryptop, crypto.c:1802-1804): with ESPGPU_EIO
+// -- which the kernel-domain driver maps to EIO, a clean drop for
+// esp_input_cb / esp_output_cb (esps_noxform, xform_esp.c:514-520) -- unless
+// its batch is seen to complete after all (then with its real result).
+// espgpu_health() reports the state: the F-Stack shim's probe then declines,
+// so new SAs go to cryptosoft, and process() refuses at once.
+
+// Wait, at most deadline_ms, for a stream's queued work; true if it drained
+// (or the device reports an error: nothing of it runs any more).
+bool stream_settle(espgpu_ctx *c, hipStream_t st) {
+  if (!st) return true;
+  const uint64_t t0 = now_ns();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q != hipErrorNotReady) return true;
+    if (now_ns() - t0 > (uint64_t)c->deadline_ms * 1000000ull) return false;
+    sched_yield();
+  }
+}
+
+// A slot's requests complete with ESPGPU_EIO (their buffers untouched: results
+// are copied back only for a batch that completed); the slot is free again.
+void drop_slot(espgpu_ctx *c, Slot &s) {
+  for (const Pending &pd : s.reqs) c->ready.push_back(espgpu_completion{pd.opaque, ESPGPU_EIO});
+  c->stats.fail_eio += s.reqs.size();
+  s.reqs.clear();
+  s.segpool.clear();
+  s.nrec = 0;
+  s.bytes = 0;
+  s.door_job = -1;
+  s.stuck = false;
+  s.state = SLOT_FREE;
+}
+
+// Mark the ctx failed (once) and release what was never handed to the
+// device: the filling slot and the host overflow.  In-flight batches are
+// retired by poll / drain (slot_check).  Returns ESPGPU_EIO.
+int ctx_fail(espgpu_ctx *c, const char *why) {
+  if (!c->failed) {
+    const std::string cause = c->err;
+    c->failed = true;
+    c->stats.gpu_fail++;
+    c->err = std::string("GPU failure: ") + why + (cause.empty() ? "" : " (" + cause + ")");
+    fprintf(stderr, "espgpu: %s; nothing more is launched, held requests complete with EIO\n", c->err.c_str());
+    if (c->door_ctl) door_stop(c);               // (failed: asks the kernel to exit, never waits)
+  }
+  for (Slot &s : c->slots)
+    if (s.state == SLOT_FILLING) drop_slot(c, s);
+  Overflow &o = c->ovf;
+  while (!o.empty()) {
+    c->ready.push_back(espgpu_completion{o.front().pd.opaque, ESPGPU_EIO});
+    c->stats.fail_eio++;
+    o.pop();
+  }
+  return ESPGPU_EIO;
+}
+
+// Where an in-flight batch stands: 1 completed, 0 still running, -1 failed
+// (its completion query returned an error, it outlived deadline_ms, or the ctx
+// failed and the batch can no longer finish).  A doorbell job of a failed ctx
+// is released only once the kernel has exited (a workgroup inside one of its
+// chunks still writes results into host memory) or after the deadline.
+int slot_check(espgpu_ctx *c, Slot &s, uint64_t now) {
+  const bool late = now > s.t_launch && now - s.t_launch > (uint64_t)c->deadline_ms * 1000000ull;
+  if (s.door_job >= 0) {
+    if (!s.stuck && door_done(c, s.door_job)) return 1;
+    if (!c->failed && !late) return 0;
+    if (!c->failed) ctx_fail(c, "doorbell job outstanding past deadline_ms");
+    return (door_exited(c) || late) ? -1 : 0;
+  }
+  hipError_t q = s.stuck ? hipErrorNotReady : hipEventQuery(s.done);
+  if (c->fault & ESPGPU_FAULT_QUERY) {
+    c->fault &= ~(uint32_t)ESPGPU_FAULT_QUERY;
+    q = hipErrorLaunchFailure;                   // injected: as a lost device reports it
+  }
+  if (q == hipSuccess) return 1;
+  if (q != hipErrorNotReady) {
+    if (!c->failed) {
+      c->err = hipGetErrorString(q);
+      ctx_fail(c, "batch completion query failed");
+    }
+    return -1;
+  }
+  if (!late) return 0;
+  if (!c->failed) ctx_fail(c, "batch outstanding past deadline_ms");
+  return -1;
+}
+
+// A slot whose launch failed part way: work already queued for it that
+// writes host memory (a self-staging kernel, the results' xfer kernel or
+// D2H copy) is waited for, boundedly, before its requests are released -- a
+// released buffer must not be written afterwards.
+int fail_launch(espgpu_ctx *c, Slot &s) {
+  if (s.wq) stream_settle(c, s.wq);
+  s.wq = nullptr;
+  return ctx_fail(c, "batch launch failed");
+}
+
 // A slot's span list of at least `need` entries (the door's fixed layout
 // keeps 3 x batch_records; a larger list moves the pinned buffer, so the
 // door kernel is stopped first and the device slot table rewritten).
@@ -610,9 +709,14 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
               uint8_t *d_status, uint8_t *d_out, uint32_t flags, int encrypt, hipStream_t st,
               uint32_t *d_trailer = nullptr, uint32_t kinds = 3, const StageLists *stage = nullptr,
               uint32_t out_stride = 0) {
+  if (c->failed) return ESPGPU_EIO;
   if (n == 0) return 0;
   if (out_stride && c->n_eta > 0)
     return fail(c, ESPGPU_ENOTSUP, "packed output serves contexts with GCM sessions only");
+  if (c->fault & ESPGPU_FAULT_LAUNCH) {
+    c->fault &= ~(uint32_t)ESPGPU_FAULT_LAUNCH;
+    return fail(c, ESPGPU_EIO, "injected launch failure");
+  }
   door_retire(c);
   if (c->launched && st != c->last_st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_last, 0));
   const uint32_t nsas = (uint32_t)c->sessions.size();
@@ -727,6 +831,11 @@ int espgpu_device_count(void) {
 
 const char *espgpu_last_error(espgpu_ctx *c) { return c ? c->err.c_str() : "no context"; }
 
+int espgpu_health(espgpu_ctx *c) {
+  if (!c) return ESPGPU_EINVAL;
+  return c->failed ? ESPGPU_EIO : ESPGPU_OK;
+}
+
 int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
   if (!out) return ESPGPU_EINVAL;
   *out = nullptr;
@@ -799,6 +908,24 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
 
 void espgpu_fini(espgpu_ctx *c) {
   if (!c) return;
+  if (c->failed) {
+    // nothing waits unboundedly on a failed device: work that may still run
+    // on it (a hung kernel) keeps its memory, which is then leaked rather
+    // than freed under it
+    bool idle = true;
+    const uint64_t t0 = now_ns();
+    while (c->door_live && !door_exited(c)) {
+      if (now_ns() - t0 > (uint64_t)c->deadline_ms * 1000000ull) { idle = false; break; }
+      sched_yield();
+    }
+    for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux}) idle = stream_settle(c, st) && idle;
+    for (auto &s : c->slots) idle = stream_settle(c, s.st) && idle;
+    if (!idle) {
+      fprintf(stderr, "espgpu_fini: device work of a failed context never finished; its memory is leaked\n");
+      delete c;
+      return;
+    }
+  }
   door_free(c);
   for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux})
     if (st) hipStreamSynchronize(st);
@@ -887,6 +1014,7 @@ int espgpu_probesession(const espgpu_session_params *csp) {
 
 int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *sid_out) {
   if (!c || !csp || !sid_out) return ESPGPU_EINVAL;
+  if (c->failed) return ESPGPU_EIO;                  // (espgpu_last_error keeps the cause)
   int pr = espgpu_probesession(csp);
   if (pr >= 0) return fail(c, ESPGPU_EINVAL, "session parameters not supported");
   const bool null_cipher = csp->csp_cipher_alg == ESPGPU_CRYPTO_NULL_CBC;
@@ -982,22 +1110,26 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
 
 void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   if (!c || sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return;
-  // Requests already staged were accepted under this key: launch them now
-  // (and the overflow behind them), then wait, so neither they nor flushed
-  // batches see the slot reused.
-  // (doorbell jobs have no stream to wait on: drain them)
-  if (c->ovf.empty() && !c->door_ctl) espgpu_flush(c);
-  else espgpu_drain(c);
-  // the doorbell kernel keeps its current session's state (H^8 table in LDS);
-  // stopped before the stream syncs, which could otherwise wait behind it
-  // on a shared hardware queue
-  door_stop(c);
-  hipStreamSynchronize(c->stream);
-  hipStreamSynchronize(c->s_out);
-  for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
-  // and the ctx's last launch on any stream: a device-resident batch on the
-  // caller's stream may still be reading this slot's keys
-  if (c->launched) hipEventSynchronize(c->ev_last);
+  if (!c->failed) {
+    // Requests already staged were accepted under this key: launch them now
+    // (and the overflow behind them), then wait, so neither they nor flushed
+    // batches see the slot reused.
+    // (doorbell jobs have no stream to wait on: drain them)
+    if (c->ovf.empty() && !c->door_ctl) espgpu_flush(c);
+    else espgpu_drain(c);
+  }
+  if (!c->failed) {
+    // the doorbell kernel keeps its current session's state (H^8 table in LDS);
+    // stopped before the stream syncs, which could otherwise wait behind it
+    // on a shared hardware queue
+    door_stop(c);
+    hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(c->s_out);
+    for (auto &sl : c->slots) hipStreamSynchronize(sl.st);
+    // and the ctx's last launch on any stream: a device-resident batch on the
+    // caller's stream may still be reading this slot's keys
+    if (c->launched) hipEventSynchronize(c->ev_last);
+  }
   const Session &fs = c->sessions[sid];
   if (fs.mode != ESPGPU_CSP_MODE_AEAD) {
     c->n_eta--;
@@ -1009,7 +1141,7 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   c->sessions[sid] = Session();
   DevSA z;
   memset(&z, 0, sizeof z);
-  hipMemcpy(c->d_sas + sid, &z, sizeof z, hipMemcpyHostToDevice);
+  if (!c->failed) hipMemcpy(c->d_sas + sid, &z, sizeof z, hipMemcpyHostToDevice);
 }
 
 // Validate that a request has the shape esp_input / esp_output build
@@ -1017,6 +1149,12 @@ void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
 int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   (void)hint;
   if (!c || !r) return ESPGPU_EINVAL;
+  if (c->failed) {
+    // never ERESTART (nothing would retry it into a working slot) nor EAGAIN:
+    // the caller completes it at once (ff_gpucrypto.c)
+    c->stats.fail_eio++;
+    return ESPGPU_EIO;
+  }
   const int op = (r->crp_op & ESPGPU_CRYPTO_OP_ENCRYPT) ? 1 : 0;
   auto reject = [&](int etype) {
     c->ready.push_back(espgpu_completion{r->opaque, etype});
@@ -1141,7 +1279,10 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
   if (!to_ovf) {
     if (slot_full(c, *s, op, rlen)) {
       int e = espgpu_flush(c);
-      if (e) return e;
+      if (e) {
+        if (c->failed) c->stats.fail_eio++;     // (this request: refused, completed by the caller)
+        return e;
+      }
       s = &c->slots[c->cur];
     }
     if (s->state == SLOT_INFLIGHT) {
@@ -1189,6 +1330,15 @@ int espgpu_process(espgpu_ctx *c, const espgpu_req *r, int hint) {
 // crypto kernels, the results out; then the next slot becomes current.
 static int launch_slot(espgpu_ctx *c, Slot &s) {
   if (s.state != SLOT_FILLING || s.nrec == 0) return 0;
+  s.wq = nullptr;
+  if (c->fault & ESPGPU_FAULT_LAUNCH) {
+    c->fault &= ~(uint32_t)ESPGPU_FAULT_LAUNCH;
+    return fail(c, ESPGPU_EIO, "injected launch failure");
+  }
+  if (c->fault & ESPGPU_FAULT_STUCK) {            // its completion will never be seen
+    c->fault &= ~(uint32_t)ESPGPU_FAULT_STUCK;
+    s.stuck = true;
+  }
   // [records][16 B slack][descriptors][status]: one H2D on s_in -> kernels on
   // the compute stream -> one D2H on s_out, chained by events, so consecutive
   // batches overlap their copies with each other's kernels.
@@ -1242,13 +1392,17 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
         }
       }
     }
-    // a kernel asked to retire (launched work went by) may still be running:
-    // cancel the request before the job is visible, then relaunch if it (or
-    // an idle timeout since the last job) ended it.  Done before the ring
-    // entry is written, so a failed relaunch leaves nothing published.
+    // A kernel asked to retire (launched work went by) may still be running.
+    // The request stands while that launched work is outstanding: the kernel
+    // then serves the jobs published meanwhile and exits, so work queued
+    // behind it on a shared hardware queue does not wait for door_idle_us.
+    // Once the launched work is done the request is cancelled before the job
+    // is visible.  A kernel that exited (the request, or an idle timeout since
+    // the last job) is relaunched, which clears it.  All before the ring entry
+    // is written, so a failed relaunch leaves nothing published.
     const uint64_t t_pub = now_ns();
     const bool was_retiring = c->door_retiring;
-    if (was_retiring) {
+    if (was_retiring && launched_idle(c)) {
       __atomic_store_n(&c->door_ctl->stop, 0u, __ATOMIC_SEQ_CST);
       c->door_retiring = false;
     }
@@ -1268,6 +1422,7 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
     s.door_t0 = t_pub;
     c->door_last_pub = t_pub;
     s.timed = false;
+    s.t_launch = now_ns();               // (the deadline counts from here: launch calls may load code)
     s.state = SLOT_INFLIGHT;
     c->stats.batches++;
     c->stats.door++;
@@ -1299,12 +1454,14 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
                          reinterpret_cast<const espgpu_desc *>(s.h_arena_dev + s.desc_off)};
     s.timed = GPU_TIME_SMALL;
     if (s.timed) hipEventRecord(s.k0, s_k);
+    s.wq = s_k;                                    // the kernel writes results to host memory
     e = run_batch(c, s.d_arena, reinterpret_cast<const espgpu_desc *>(s.d_arena + s.desc_off), s.nrec,
                   dres + s.stat_off, s.op ? nullptr : s.d_out, (uint32_t)ESPGPU_BATCH_GROUPED, s.op, s_k,
                   nullptr, 1u, &stg);
     if (e) return e;
     if (s.timed) hipEventRecord(s.k1, s_k);
     HIPCHK(c, hipEventRecord(s.done, s_k));
+    s.t_launch = now_ns();               // (the deadline counts from here: launch calls may load code)
     s.state = SLOT_INFLIGHT;
     c->stats.batches++;
     c->stats.zerocopy += s.nrec - s.nstaged;
@@ -1372,6 +1529,7 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
                     s.op, s_k, nullptr, s.kinds);
   if (e) return e;
   if (s.timed) hipEventRecord(s.k1, s_k);
+  if (nout) s.wq = s_k;                          // results to host memory (zero-copy / staging)
   if (nout && launch_xfer(s.h_xfer_dev + nin, nout, d_stat, s_k)) return fail(c, ESPGPU_EIO, "xfer kernel launch failed");
   if (!kcopy) {
     if (!small) {
@@ -1381,6 +1539,7 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
     HIPCHK(c, hipMemcpyAsync(s.h_arena + out_lo, dres + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, s_out));
   }
   HIPCHK(c, hipEventRecord(s.done, kcopy ? s_k : s_out));
+  s.t_launch = now_ns();
   s.state = SLOT_INFLIGHT;
   c->stats.batches++;
   c->stats.zerocopy += s.nrec - s.nstaged;
@@ -1390,13 +1549,15 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
 
 int espgpu_flush(espgpu_ctx *c) {
   if (!c) return ESPGPU_EINVAL;
+  if (c->failed) return ESPGPU_EIO;
   // the filling slot, then the overflow (oldest first) into the free slots
   Overflow &o = c->ovf;
   for (;;) {
     Slot &s = c->slots[c->cur];
     if (s.state == SLOT_FILLING) {
-      int e = launch_slot(c, s);
-      if (e) return e;
+      // a batch that cannot be launched is a GPU failure: its requests, the
+      // overflow's and (through poll) the in-flight ones complete with EIO
+      if (launch_slot(c, s)) return fail_launch(c, s);
       continue;
     }
     if (o.empty() || s.state != SLOT_FREE) break;
@@ -1446,29 +1607,29 @@ int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
   // completions of flushed batches, oldest first, and in arrival order: a
   // batch that finished before an older one (another stream's kernel, a
   // doorbell job another workgroup took) waits for it
+  // (a batch whose completion fails, or that outlives deadline_ms, fails the
+  // ctx and completes with EIO: slot_check)
   bool door_wait = false;
-  const uint64_t now = c->door_ctl ? now_ns() : 0;
+  const uint64_t now = now_ns();
   for (size_t k = 0; k < c->slots.size(); ++k) {
     Slot &s = c->slots[(c->cur + k) % c->slots.size()];
     if (s.state != SLOT_INFLIGHT) continue;
-    if (s.door_job >= 0) {
-      if (!door_done(c, s.door_job)) {
-        // outstanding for over 100 us: make sure the kernel is still there
-        // (a workgroup that read a retire request just before the job was
-        // published may have exited with it)
-        door_wait = now - s.door_t0 > 100000u;
-        break;
-      }
-      s.door_job = -1;
-    } else if (hipEventQuery(s.done) != hipSuccess) {
+    const int r = slot_check(c, s, now);
+    if (r == 0) {
+      // a doorbell job outstanding for over 100 us: make sure the kernel is
+      // still there (a workgroup that read a retire request just before the
+      // job was published may have exited with it)
+      door_wait = s.door_job >= 0 && now - s.door_t0 > 100000u;
       break;
     }
+    if (r < 0) {
+      drop_slot(c, s);
+      continue;
+    }
+    s.door_job = -1;
     complete_slot(c, s);
   }
-  if (door_wait) {
-    int e = door_ensure(c);
-    if (e) return -e;
-  }
+  if (door_wait && !c->failed && door_ensure(c)) ctx_fail(c, "door kernel relaunch failed");
   const int avail = (int)(c->ready.size() - c->ready_head);
   const int n = std::min(max, avail);
   for (int i = 0; i < n; ++i) out[i] = c->ready[c->ready_head + i];
@@ -1483,29 +1644,28 @@ int espgpu_poll(espgpu_ctx *c, espgpu_completion *out, int max) {
 int espgpu_drain(espgpu_ctx *c) {
   if (!c) return ESPGPU_EINVAL;
   do {
-    int e = espgpu_flush(c);
-    if (e) return e;
-    // oldest first (slot cur is the next to fill, so cur+1.. are older batches)
+    espgpu_flush(c);              // (a launch failure fails the ctx: the loop below retires the rest)
+    // oldest first (slot cur is the next to fill, so cur+1.. are older
+    // batches); every wait is bounded by deadline_ms (slot_check), so a
+    // batch the GPU never finishes completes with EIO instead of hanging
     for (size_t k = 0; k < c->slots.size(); ++k) {
       Slot &s = c->slots[(c->cur + k) % c->slots.size()];
       if (s.state != SLOT_INFLIGHT) continue;
-      if (s.door_job >= 0) {
-        // the persistent kernel's job: spin on done[], relaunching the
-        // kernel if it exited; a job the GPU never finishes is an error
-        const uint64_t t0 = now_ns();
-        while (!door_done(c, s.door_job)) {
-          int e = door_ensure(c);
-          if (e) return e;
-          if (now_ns() - t0 > 10000000000ull) return fail(c, ESPGPU_EIO, "door job %lld not done after 10 s", (long long)s.door_job);
-        }
-        s.door_job = -1;
-      } else {
-        HIPCHK(c, hipEventSynchronize(s.done));
+      int r;
+      while ((r = slot_check(c, s, now_ns())) == 0) {
+        // the persistent kernel's job: relaunch the kernel if it exited
+        if (s.door_job >= 0 && !c->failed && door_ensure(c)) ctx_fail(c, "door kernel relaunch failed");
+        sched_yield();
       }
+      if (r < 0) {
+        drop_slot(c, s);
+        continue;
+      }
+      s.door_job = -1;
       complete_slot(c, s);
     }
   } while (!c->ovf.empty());     // the overflow goes into the slots just freed
-  return 0;
+  return c->failed ? ESPGPU_EIO : 0;
 }
 
 int espgpu_register_host(espgpu_ctx *c, void *base, uint64_t len) {
@@ -1627,19 +1787,26 @@ int espgpu_get_stats(espgpu_ctx *c, espgpu_stats *st) {
   return 0;
 }
 
+// The device-resident entry points: a launch that could not be queued (EIO)
+// fails the ctx as a process-path launch does (later calls answer EIO).
+static int batch_rc(espgpu_ctx *c, int e) {
+  if (e == ESPGPU_EIO && !c->failed) ctx_fail(c, "batch launch failed");
+  return e;
+}
+
 int espgpu_decrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
                          uint8_t *d_status, uint8_t *d_out, uint32_t flags, void *stream) {
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return ESPGPU_EINVAL;
-  return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
-                   reinterpret_cast<hipStream_t>(stream));
+  return batch_rc(c, run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
+                             reinterpret_cast<hipStream_t>(stream)));
 }
 
 int espgpu_decrypt_batch_trailer(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc,
                                  uint32_t n, uint8_t *d_status, uint8_t *d_out, uint32_t *d_trailer,
                                  uint32_t flags, void *stream) {
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_trailer && n)) return ESPGPU_EINVAL;
-  return run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
-                   reinterpret_cast<hipStream_t>(stream), d_trailer);
+  return batch_rc(c, run_batch(c, d_arena, d_desc, n, d_status, d_out ? d_out : d_arena, flags, 0,
+                             reinterpret_cast<hipStream_t>(stream), d_trailer));
 }
 
 int espgpu_decrypt_batch_packed(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
@@ -1648,14 +1815,14 @@ int espgpu_decrypt_batch_packed(espgpu_ctx *c, uint8_t *d_arena, const espgpu_de
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n) || (!d_out && n) || d_out == d_arena ||
       out_stride == 0 || out_stride % 128 != 0 || ((uintptr_t)d_out & 127))
     return ESPGPU_EINVAL;
-  return run_batch(c, d_arena, d_desc, n, d_status, d_out, flags, 0, reinterpret_cast<hipStream_t>(stream),
-                   nullptr, 3, nullptr, out_stride);
+  return batch_rc(c, run_batch(c, d_arena, d_desc, n, d_status, d_out, flags, 0, reinterpret_cast<hipStream_t>(stream),
+                             nullptr, 3, nullptr, out_stride));
 }
 
 int espgpu_encrypt_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32_t n,
                          uint8_t *d_status, uint32_t flags, void *stream) {
   if (!c || (!d_arena && n) || (!d_desc && n) || (!d_status && n)) return ESPGPU_EINVAL;
-  return run_batch(c, d_arena, d_desc, n, d_status, nullptr, flags, 1, reinterpret_cast<hipStream_t>(stream));
+  return batch_rc(c, run_batch(c, d_arena, d_desc, n, d_status, nullptr, flags, 1, reinterpret_cast<hipStream_t>(stream)));
 }
 
 float espgpu_last_kernel_ms(espgpu_ctx *c) { return c ? c->last_ms : 0.f; }
@@ -1708,7 +1875,8 @@ static int host_pipeline(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_b
 int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_bytes,
                         const espgpu_desc *h_desc, uint32_t n, uint8_t *h_status, uint8_t *h_out,
                         uint32_t chunk, uint32_t flags) {
-  return host_pipeline(c, h_arena, arena_bytes, h_desc, n, h_status, h_out, chunk, flags, 0);
+  if (c && c->failed) return ESPGPU_EIO;
+  return batch_rc(c, host_pipeline(c, h_arena, arena_bytes, h_desc, n, h_status, h_out, chunk, flags, 0));
 }
 
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
@@ -1750,8 +1918,22 @@ int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
       int e = espgpu_drain(c);
       if (e) return e;
     }
+    // all three rings or none: on ENOMEM the previous overflow stays
+    if (!c->ovf.init((size_t)value << 20))
+      return fail(c, ESPGPU_ENOMEM, "overflow_mb %d: host allocation failed", value);
     c->ovf_cap = (size_t)value << 20;
-    c->ovf.init(c->ovf_cap);
+    return 0;
+  }
+  if (!strcmp(key, "fault")) {
+    // fault injection (tests of the GPU-failure path): ESPGPU_FAULT_* bits,
+    // each consumed by the next launch / completion query / launched batch
+    if (value & ~(ESPGPU_FAULT_LAUNCH | ESPGPU_FAULT_QUERY | ESPGPU_FAULT_STUCK)) return ESPGPU_EINVAL;
+    c->fault = (uint32_t)value;
+    return 0;
+  }
+  if (!strcmp(key, "deadline_ms")) {
+    if (value < 1 || value > 600000) return ESPGPU_EINVAL;
+    c->deadline_ms = (uint32_t)value;
     return 0;
   }
   if (!strcmp(key, "gcm_burst")) {

@@ -38,9 +38,11 @@ TR_BADLEN = 0x00010000
 TR_BADPAD = 0x00020000
 TR_NONE = 0x00040000
 TR_VALID = 0x80000000
+EIO = 5
 EINVAL = 22
 EBADMSG = 74
 ERESTART = 85
+FAULT_LAUNCH, FAULT_QUERY, FAULT_STUCK = 0x1, 0x2, 0x4   # set_tuning "fault" (espgpu.h)
 
 
 class SessionParams(C.Structure):
@@ -94,7 +96,7 @@ class Stats(C.Structure):
                 ("einval", C.c_uint64), ("batches", C.c_uint64), ("kernel_ns", C.c_uint64),
                 ("erestart", C.c_uint64), ("overflow", C.c_uint64), ("zerocopy", C.c_uint64),
                 ("door", C.c_uint64), ("ovf_reserved", C.c_uint64), ("ovf_peak", C.c_uint64),
-                ("ovf_process_ns_max", C.c_uint64)]
+                ("ovf_process_ns_max", C.c_uint64), ("gpu_fail", C.c_uint64), ("fail_eio", C.c_uint64)]
 
 
 _lib = None
@@ -124,6 +126,7 @@ def lib():
         L.espgpu_fini.restype = None
         L.espgpu_last_error.argtypes = [vp]
         L.espgpu_last_error.restype = C.c_char_p
+        L.espgpu_health.argtypes = [vp]
         L.espgpu_probesession.argtypes = [C.POINTER(SessionParams)]
         L.espgpu_newsession.argtypes = [vp, C.POINTER(SessionParams), C.POINTER(C.c_int32)]
         L.espgpu_freesession.argtypes = [vp, C.c_int32]

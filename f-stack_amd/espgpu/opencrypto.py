@@ -18,7 +18,7 @@ import itertools
 
 from . import _lib as L
 from ._lib import (CRYPTO_F_IV_SEPARATE, CSP_MODE_AEAD, CSP_MODE_ETA, EINVAL,  # noqa: F401
-                   ERESTART)
+                   EIO, ERESTART)
 
 CRYPTO_F_DONE = 0x0020
 EOPNOTSUPP = 95
@@ -163,10 +163,16 @@ class GpuCryptoDriver:
             self._inflight[tok] = (crp, segs, keep)
         return rc
 
+    def health(self):
+        """0, or EIO once the GPU failed (espgpu_health)"""
+        return self.lib.espgpu_health(self.ctx)
+
     def flush(self):
         rc = self.lib.espgpu_flush(self.ctx)
-        if rc:
+        # EIO: the GPU failed; the held requests come back through poll()
+        if rc and rc != EIO:
             raise RuntimeError("espgpu_flush: %s" % self.last_error())
+        return rc
 
     def poll(self, max_n=4096):
         out = (L.Completion * max_n)()
@@ -180,8 +186,9 @@ class GpuCryptoDriver:
 
     def drain(self):
         rc = self.lib.espgpu_drain(self.ctx)
-        if rc:
+        if rc and rc != EIO:
             raise RuntimeError("espgpu_drain: %s" % self.last_error())
+        return rc
 
     def set_tuning(self, key, value):
         return self.lib.espgpu_set_tuning(self.ctx, key.encode(), value)
@@ -243,7 +250,12 @@ class CryptoFramework:
         if rc == ERESTART:
             self._blocked.append(crp)
             return 0
-        return rc
+        if rc:
+            # a request the engine refuses (EIO once the GPU failed) completes
+            # at once, as the kernel-domain driver's gpucrypto_fail does
+            crp.crp_etype = rc
+            self._done([crp])
+        return 0
 
     def _done(self, crps):
         for crp in crps:
@@ -259,9 +271,14 @@ class CryptoFramework:
         self._done(done)
         # crypto_unblock: retry queued requests now that a slot may be free
         while self._blocked:
-            if self.driver.process(self._blocked[0]) == ERESTART:
+            crp = self._blocked[0]
+            rc = self.driver.process(crp)
+            if rc == ERESTART:
                 break
             self._blocked.pop(0)
+            if rc:
+                crp.crp_etype = rc
+                self._done([crp])
         return len(done)
 
     def crypto_drain(self):

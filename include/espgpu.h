@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define ESPGPU_ABI_VERSION 4
+#define ESPGPU_ABI_VERSION 5
 
 /* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
 #define ESPGPU_CSP_MODE_CIPHER      2        /* cryptodev.h:362: ESP without auth */
@@ -133,7 +133,7 @@ struct espgpu_req {
 
 struct espgpu_completion {
 	void *opaque;
-	int   etype;            /* crp_etype: 0, EBADMSG, EINVAL, ENOMEM, EAGAIN */
+	int   etype;            /* crp_etype: 0, EBADMSG, EINVAL, EIO (GPU failure) */
 };
 
 /* Device-resident descriptor: one per ESP record (16 bytes). */
@@ -165,6 +165,8 @@ struct espgpu_stats {
 	                                  set once by set_tuning "overflow_mb", never grown */
 	uint64_t ovf_peak;             /* most record bytes the overflow held at once    */
 	uint64_t ovf_process_ns_max;   /* longest overflow placement inside process()    */
+	uint64_t gpu_fail;             /* GPU failures detected (ABI 5): 0, or 1 once failed */
+	uint64_t fail_eio;             /* requests completed or refused with EIO because of it */
 };
 
 typedef struct espgpu_ctx espgpu_ctx;
@@ -179,6 +181,17 @@ int  espgpu_device_count(void);
 int  espgpu_init(const struct espgpu_config *cfg, espgpu_ctx **out);
 void espgpu_fini(espgpu_ctx *ctx);
 const char *espgpu_last_error(espgpu_ctx *ctx);
+/* GPU health: ESPGPU_OK, or ESPGPU_EIO once the context has seen a GPU
+ * failure -- a launch or copy that could not be queued, a completion query
+ * that returned an error, or a batch outstanding longer than set_tuning
+ * "deadline_ms" (default 2000).  From then on the context launches nothing:
+ * every request it held completes exactly once through espgpu_poll with
+ * etype ESPGPU_EIO (unless its batch is seen to complete after all),
+ * espgpu_process / flush / drain / newsession and the batch entry points
+ * answer ESPGPU_EIO, and espgpu_last_error names the cause.  The F-Stack
+ * shim's probe declines on a failed context, so new sessions go to
+ * cryptosoft. */
+int  espgpu_health(espgpu_ctx *ctx);
 
 /* ---- opencrypto driver methods (cryptodev_if.m) ---- */
 /* CRYPTODEV_PROBESESSION (cryptodev_if.m:72-75): ESPGPU_PROBE_HARDWARE or EINVAL.
@@ -190,7 +203,9 @@ int  espgpu_newsession(espgpu_ctx *ctx, const struct espgpu_session_params *csp,
                        int32_t *session_out);
 /* CRYPTODEV_FREESESSION (cryptodev_if.m:113-116) */
 void espgpu_freesession(espgpu_ctx *ctx, int32_t session);
-/* CRYPTODEV_PROCESS (cryptodev_if.m:143-147): never blocks.  Stages the
+/* CRYPTODEV_PROCESS (cryptodev_if.m:143-147): never blocks.  On a failed
+ * context (espgpu_health) it answers ESPGPU_EIO at once: never ERESTART or
+ * EAGAIN, which would hand the request back to this dead engine.  Stages the
  * request; returns 0, or ERESTART when every staging slot is in flight (the
  * framework then sets cc_qblocked and requeues, crypto.c:1451-1459).  With
  * set_tuning "overflow_mb" > 0 such a request is kept in a host overflow
@@ -388,10 +403,20 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *   "stage_fused" a process-path burst of one GCM session stages its own
  *               records inside the crypto kernel (1, default: one launch per
  *               burst) instead of xfer kernels around it (0);
+ *   "deadline_ms" a batch outstanding this long (launch to completion) is a
+ *               GPU failure (espgpu_health); 1..600000, default 2000;
+ *   "fault"     fault injection for the GPU-failure path's tests: a mask of
+ *               ESPGPU_FAULT_LAUNCH (the next launch fails), _QUERY (the next
+ *               completion query of an in-flight batch returns an error) and
+ *               _STUCK (the next batch launched is never seen to complete, so
+ *               it meets the deadline); each bit is consumed once;
  *   "gcm_opts" / "eta_opts" measurement knobs that skip work on purpose
  *               (results wrong): only in libespgpu_knobs.so, ENOTSUP in the
  *               product library unless 0.
  * Returns 0, EINVAL, ENOTSUP or ENOENT (unknown key). */
+#define ESPGPU_FAULT_LAUNCH 0x1
+#define ESPGPU_FAULT_QUERY  0x2
+#define ESPGPU_FAULT_STUCK  0x4
 int  espgpu_set_tuning(espgpu_ctx *ctx, const char *key, int value);
 
 #ifdef __cplusplus

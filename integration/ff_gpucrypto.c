@@ -21,6 +21,11 @@
  *                 queues the request and blocks the driver until
  *                 crypto_unblock); every other failure completes the request
  *                 through crypto_done with crp_etype set, as swcr_process does.
+ *   GPU failure   requests the engine held complete with EIO (a clean drop);
+ *                 later ones move their session to cryptosoft
+ *                 (gpucrypto_migrate: EAGAIN with a new session, the
+ *                 framework's own CRYPTOCAP_F_CLEANUP protocol); the probe
+ *                 declines, so new sessions go to cryptosoft.
  * Completions come back on the lcore thread from ff_gpucrypto_poll() (host
  * domain, main_loop) through ff_gpucrypto_done() below.
  *
@@ -60,6 +65,7 @@ int  ff_gpucrypto_host_probe(const struct espgpu_session_params *csp);
 int  ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid);
 void ff_gpucrypto_host_freesession(int32_t sid);
 int  ff_gpucrypto_host_process(const struct espgpu_req *r, int hint);
+int  ff_gpucrypto_host_failed(void);
 
 /* kernel-domain entry points the host domain calls (lib/ff_api.symlist) */
 void ff_gpucrypto_done(void *opaque, int abi_etype);
@@ -75,6 +81,7 @@ gpucrypto_errno(int abi)
 {
 	switch (abi) {
 	case ESPGPU_OK:       return (0);
+	case ESPGPU_EIO:      return (EIO);          /* GPU failure: a clean drop */
 	case ESPGPU_EINVAL:   return (EINVAL);
 	case ESPGPU_EBADMSG:  return (EBADMSG);      /* 89 */
 	case ESPGPU_ERESTART: return (ERESTART);     /* -1 */
@@ -145,6 +152,40 @@ gpucrypto_fail(struct cryptop *crp, int error)
 	return (0);
 }
 
+/*
+ * The GPU failed (the engine's espgpu_health; its held requests complete
+ * with EIO through ff_gpucrypto_done).  This driver cannot unregister:
+ * crypto_unregister_all waits in mtx_sleep until the driver's sessions are
+ * gone (crypto.c:1178-1179) and F-Stack's _sleep returns at once
+ * (lib/ff_kern_synch.c:87-92), so it would spin forever.  Instead it does for
+ * each of its sessions, on that session's next request, what crypto_invoke
+ * does for a driver that did unregister (the CRYPTOCAP_F_CLEANUP branch,
+ * crypto.c:1684-1725): a new session on the same parameters -- the probe
+ * now declines, so crypto_newsession selects cryptosoft -- goes into the
+ * request, which completes with EAGAIN; esp_input_cb / esp_output_cb then
+ * move the SA to that session and re-dispatch (xform_esp.c:505-512,
+ * ipsec_updateid ipsec.c:1451-1495).  Unlike that branch the old session is
+ * not freed here (its requests still held by the engine complete with EIO,
+ * and a second request naming it would free it twice): once the SA has moved
+ * nothing uses it, and it is left, one per SA.  Without another driver, or
+ * should the new session land on this one, the request is a clean drop (EIO).
+ */
+static int
+gpucrypto_migrate(struct cryptop *crp)
+{
+	crypto_session_t nses;
+
+	if (crypto_newsession(&nses, crypto_get_params(crp->crp_session),
+	    CRYPTOCAP_F_HARDWARE | CRYPTOCAP_F_SOFTWARE) != 0)
+		return (gpucrypto_fail(crp, EIO));
+	if (gpucrypto_id >= 0 && crypto_ses2hid(nses) == (uint32_t)gpucrypto_id) {
+		crypto_freesession(nses);
+		return (gpucrypto_fail(crp, EIO));
+	}
+	crp->crp_session = nses;
+	return (gpucrypto_fail(crp, EAGAIN));
+}
+
 static int
 gpucrypto_process(device_t dev, struct cryptop *crp, int hint)
 {
@@ -155,6 +196,8 @@ gpucrypto_process(device_t dev, struct cryptop *crp, int hint)
 	int n = 0, e;
 
 	(void)dev;
+	if (ff_gpucrypto_host_failed())
+		return (gpucrypto_migrate(crp));
 	/* in place only; session keys only (ESP never rekeys per request) */
 	if (CRYPTO_HAS_OUTPUT_BUFFER(crp) || crp->crp_cipher_key != NULL ||
 	    crp->crp_auth_key != NULL)
@@ -199,6 +242,8 @@ gpucrypto_process(device_t dev, struct cryptop *crp, int hint)
 		return (0);
 	if (e == ESPGPU_ERESTART)
 		return (ERESTART);                  /* framework queues + blocks */
+	if (e == ESPGPU_EIO && ff_gpucrypto_host_failed())
+		return (gpucrypto_migrate(crp));    /* the GPU failed under this request */
 	return (gpucrypto_fail(crp, gpucrypto_errno(e)));
 }
 

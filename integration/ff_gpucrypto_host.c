@@ -122,15 +122,26 @@ int ff_gpucrypto_host_tune(const char *key, int value)
 	return g_ctx ? espgpu_set_tuning(g_ctx, key, value) : ESPGPU_ENXIO;
 }
 
-/* CRYPTODEV_PROBESESSION: -100 (CRYPTODEV_PROBE_HARDWARE) or EINVAL.
+/* the GPU context has failed (espgpu_health): the driver stops taking work */
+int ff_gpucrypto_host_failed(void)
+{
+	return g_ctx != NULL && espgpu_health(g_ctx) != ESPGPU_OK;
+}
+
+/* CRYPTODEV_PROBESESSION: -100 (CRYPTODEV_PROBE_HARDWARE) or EINVAL; ENXIO
+ * once the GPU has failed, so crypto_newsession picks cryptosoft.
  * Host-only, valid before ff_gpucrypto_host_init. */
 int ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
 {
+	if (ff_gpucrypto_host_failed())
+		return ESPGPU_ENXIO;
 	return espgpu_probesession(csp);
 }
 
 int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid)
 {
+	if (ff_gpucrypto_host_failed())
+		return ESPGPU_ENXIO;
 	return g_ctx ? espgpu_newsession(g_ctx, csp, sid) : ESPGPU_ENXIO;
 }
 
@@ -141,7 +152,8 @@ void ff_gpucrypto_host_freesession(int32_t sid)
 }
 
 /* CRYPTODEV_PROCESS: ESPGPU_OK or ESPGPU_ERESTART (the driver returns
- * ERESTART and the framework requeues); the driver maps any other code */
+ * ERESTART and the framework requeues); the driver maps any other code
+ * (ESPGPU_EIO on a failed GPU: the driver then moves the session) */
 int ff_gpucrypto_host_process(const struct espgpu_req *r, int hint)
 {
 	int e;

@@ -35,7 +35,7 @@ RUN = os.path.join(HERE, "fstack_run")
 EXE_CPU = os.path.join(HERE, "fstack_crypto_run_cpu")
 EXE_GPU = os.path.join(HERE, "fstack_crypto_run_gpu")
 EXPORTS = ["ffst_find_driver", "ffst_newsession", "ffst_freesession", "ffst_request", "ffst_dispatch",
-           "ffst_result", "ffst_free"]
+           "ffst_result", "ffst_ndone", "ffst_redispatch", "ffst_free"]
 SELFTEST_RULE = """
 ff_crypto_selftest.o: ff_crypto_selftest.c $(IMACROS_FILE)
 \t${NORMAL_C}
@@ -121,10 +121,12 @@ def pack_requests(path, sessions, requests):
             f.write(bytes(r["buf"]))
 
 
-def read_results(path, lens):
+def read_results(path, lens, fail=False):
     """-> (gpu_hid, sw_hid, sessions [(err_def, hid_def, err_sw, hid_sw)],
     requests [dict etype, done_flag, buf, etype_sw, done_flag_sw, buf_sw,
-    dispatch, dispatch_sw])"""
+    dispatch, dispatch_sw]; with fail (host_main.c --fail) also f1_dispatch,
+    f1_ndone, f1_etype, f1_buf (held when the GPU failed), f2_redispatch,
+    f2_etype0, f2_hid, f2_ndone, f2_etype, f2_buf (dispatched after it)]"""
     with open(path, "rb") as f:
         magic, nses, nreq, gh, sh = struct.unpack("<IIIii", f.read(20))
         assert magic == 0x53525346 and nreq == len(lens)
@@ -133,8 +135,13 @@ def read_results(path, lens):
         for n in lens:
             v = struct.unpack("<6i", f.read(24))
             b0, b1 = f.read(n), f.read(n)
-            reqs.append(dict(etype=v[0], done_flag=v[1], buf=b0, etype_sw=v[2], done_flag_sw=v[3], buf_sw=b1,
-                             dispatch=v[4], dispatch_sw=v[5]))
+            d = dict(etype=v[0], done_flag=v[1], buf=b0, etype_sw=v[2], done_flag_sw=v[3], buf_sw=b1,
+                     dispatch=v[4], dispatch_sw=v[5])
+            if fail:
+                w = struct.unpack("<8i", f.read(32))
+                d.update(f1_dispatch=w[0], f1_ndone=w[1], f1_etype=w[2], f2_redispatch=w[3], f2_etype0=w[4],
+                         f2_hid=w[5], f2_ndone=w[6], f2_etype=w[7], f1_buf=f.read(n), f2_buf=f.read(n))
+            reqs.append(d)
     return gh, sh, ses, reqs
 
 

@@ -19,6 +19,9 @@
  *   ffst_result       the callback's record: crypto_done ran it inline
  *                     (CRYPTO_F_CBIFSYNC and a CRYPTOCAP_F_SYNC driver,
  *                     crypto.c:1802-1826), and m_copydata of the result
+ *   ffst_redispatch   esp_input_cb's EAGAIN path (xform_esp.c:505-512): the
+ *                     request names the session the driver moved it to;
+ *                     crypto_dispatch it again (the GPU-failure phase)
  * The host half (host_main.c) drives these after ff_freebsd_init().
  */
 #include <sys/param.h>
@@ -35,6 +38,8 @@ void *ffst_request(void *ses, const int *f, const void *aad, const void *esn, co
     const void *buf, int len, const int *cuts, int ncuts);
 int   ffst_dispatch(void *r);
 int   ffst_result(void *r, void *out, int len, int *flags);
+int   ffst_ndone(void *r);
+int   ffst_redispatch(void *r, int *etype0, int *hid);
 void  ffst_free(void *r);
 
 struct ffst_req {
@@ -43,7 +48,9 @@ struct ffst_req {
 	char		*buf;
 	int		 len;
 	int		 done;		/* the callback ran */
+	int		 ndone;		/* how many times */
 	int		 done_flag;	/* CRYPTO_F_DONE was set when it ran */
+	crypto_session_t moved;	/* the session a GPU failure moved it to (freed with it) */
 	uint8_t		 aad[16];
 };
 
@@ -54,6 +61,7 @@ ffst_cb(struct cryptop *crp)
 
 	r->done_flag = (crp->crp_flags & CRYPTO_F_DONE) != 0;
 	r->done = 1;
+	r->ndone++;
 	return (0);
 }
 
@@ -190,6 +198,32 @@ ffst_result(void *rp, void *out, int len, int *flags)
 	return (r->crp->crp_etype);
 }
 
+int
+ffst_ndone(void *rp)
+{
+	return (((struct ffst_req *)rp)->ndone);
+}
+
+/* The request completed with EAGAIN and a new session (gpucrypto_migrate):
+ * what esp_input_cb does next -- dispatch it again on that session.  The
+ * request's own session becomes the moved one (freed with the request: here
+ * no SA keeps it, as ipsec_updateid would). */
+int
+ffst_redispatch(void *rp, int *etype0, int *hid)
+{
+	struct ffst_req *r = rp;
+
+	*etype0 = r->crp->crp_etype;
+	*hid = (int)crypto_ses2hid(r->crp->crp_session);
+	if (r->crp->crp_etype != EAGAIN)
+		return (-1);
+	r->moved = r->crp->crp_session;
+	r->done = 0;
+	r->crp->crp_etype = 0;
+	r->crp->crp_flags &= ~CRYPTO_F_DONE;
+	return (crypto_dispatch(r->crp));
+}
+
 void
 ffst_free(void *rp)
 {
@@ -197,6 +231,8 @@ ffst_free(void *rp)
 
 	if (r->crp != NULL)
 		crypto_freereq(r->crp);
+	if (r->moved != NULL)
+		crypto_freesession(r->moved);
 	if (r->m != NULL)
 		m_freem(r->m);
 	if (r->buf != NULL)

@@ -17,9 +17,17 @@
  *      (cryptosoft, the reference path itself);
  *   4. every request crypto_dispatch'ed on both (mbuf chains or contiguous
  *      buffers), main_loop's ff_gpucrypto_poll() until each callback has run
- *      (crypto_done inline: no crypto_ret thread runs in F-Stack).
+ *      (crypto_done inline: no crypto_ret thread runs in F-Stack);
+ *   5. with --fail, the GPU-failure path: the engine
+ *      fails (GPU build: set_tuning "fault" 1, the next launch fails; CPU
+ *      build: the stand-in fails with the requests staged), every request is
+ *      dispatched again on the gpucrypto sessions and must complete exactly
+ *      once, with EIO and its buffer untouched; then once more: each now
+ *      completes with EAGAIN and a cryptosoft session (gpucrypto_migrate,
+ *      the framework's CRYPTOCAP_F_CLEANUP protocol), and its re-dispatch
+ *      (esp_input_cb's EAGAIN path) runs on cryptosoft.
  *
- *   fstack_crypto_run <requests.bin> <results.bin>
+ *   fstack_crypto_run <requests.bin> <results.bin> [--fail]
  * File formats: integration/fstack_run.py (pack_requests / read_results).
  */
 #include <stdint.h>
@@ -41,14 +49,19 @@ void *ffst_request(void *ses, const int *f, const void *aad, const void *esn, co
     const void *buf, int len, const int *cuts, int ncuts);
 int   ffst_dispatch(void *r);
 int   ffst_result(void *r, void *out, int len, int *flags);
+int   ffst_ndone(void *r);
+int   ffst_redispatch(void *r, int *etype0, int *hid);
 void  ffst_free(void *r);
 int   ff_gpucrypto_poll(void);
+int   ff_gpucrypto_host_failed(void);
 
 #ifdef FSR_GPU
 int ff_gpucrypto_host_init_proc(int proc_id);
 void ff_gpucrypto_host_fini(void);
+int ff_gpucrypto_host_tune(const char *key, int value);
 #else
 void oracle_engine_init(void);
+void oracle_engine_fail(void);
 #endif
 
 struct ses_rec {                  /* 8 ints, 32 + 128 key bytes */
@@ -90,8 +103,9 @@ main(int argc, char **argv)
 	FILE *in, *out;
 	uint32_t magic, nses, nreq;
 
-	if (argc != 3)
-		die("usage: fstack_crypto_run <requests.bin> <results.bin>");
+	const int fail = argc == 4 && strcmp(argv[3], "--fail") == 0;
+	if (argc != 3 && !fail)
+		die("usage: fstack_crypto_run <requests.bin> <results.bin> [--fail]");
 	in = fopen(argv[1], "rb");
 	if (in == NULL)
 		die("cannot open requests");
@@ -169,6 +183,58 @@ main(int argc, char **argv)
 		disp[2 * i + 1] = ffst_dispatch(rsw[i]);
 	}
 
+	/* 5. the GPU-failure phase: f1 = the requests the engine holds when it
+	 * fails, f2 = requests after it */
+	void **rf1 = calloc(nreq, sizeof(void *)), **rf2 = calloc(nreq, sizeof(void *));
+	int32_t *fv = calloc(6 * (size_t)nreq, sizeof(int32_t));
+	if (fail) {
+#ifdef FSR_GPU
+		if (ff_gpucrypto_host_tune("fault", 1) != 0)
+			die("fault injection refused");
+#endif
+		for (uint32_t i = 0; i < nreq; i++) {
+			if (sdef[rh[i].ses] == NULL || sinfo[4 * rh[i].ses + 1] != gpu_hid)
+				continue;
+			rf1[i] = ffst_request(sdef[rh[i].ses], rh[i].f, rh[i].aad, rh[i].esn, rh[i].iv, bufs[i],
+			    rh[i].len, rh[i].cuts, rh[i].ncuts);
+			if (rf1[i] == NULL)
+				die("request");
+			fv[6 * i] = ffst_dispatch(rf1[i]);
+		}
+#ifndef FSR_GPU
+		oracle_engine_fail();
+#endif
+		double t1 = now();
+		for (;;) {
+			int pending = 0, fl;
+			for (uint32_t i = 0; i < nreq; i++)
+				if (rf1[i] && ffst_result(rf1[i], tmp, 0, &fl) < 0)
+					pending++;
+			if (!pending)
+				break;
+			ff_gpucrypto_poll();
+			if (now() - t1 > 30)
+				die("requests held at the failure did not complete");
+		}
+		for (int k = 0; k < 16; k++)           /* more main-loop iterations deliver nothing twice */
+			ff_gpucrypto_poll();
+		if (!ff_gpucrypto_host_failed())
+			die("the engine does not report the failure");
+		for (uint32_t i = 0; i < nreq; i++) {
+			if (rf1[i] == NULL)
+				continue;
+			fv[6 * i + 1] = ffst_ndone(rf1[i]);
+			rf2[i] = ffst_request(sdef[rh[i].ses], rh[i].f, rh[i].aad, rh[i].esn, rh[i].iv, bufs[i],
+			    rh[i].len, rh[i].cuts, rh[i].ncuts);
+			if (rf2[i] == NULL)
+				die("request");
+			if (ffst_dispatch(rf2[i]) != 0)                /* completes at once (EAGAIN) */
+				die("dispatch after the failure");
+			fv[6 * i + 2] = ffst_redispatch(rf2[i], &fv[6 * i + 3], &fv[6 * i + 4]);
+			fv[6 * i + 5] = ffst_ndone(rf2[i]);
+		}
+	}
+
 	out = fopen(argv[2], "wb");
 	if (out == NULL)
 		die("cannot open results");
@@ -189,6 +255,27 @@ main(int argc, char **argv)
 		fwrite(v, 4, 6, out);
 		fwrite(b0, 1, (size_t)rh[i].len, out);
 		fwrite(b1, 1, (size_t)rh[i].len, out);
+		if (fail) {
+			/* f1: dispatch, crypto_done calls, etype, buffer; f2: redispatch rc,
+			 * etype before it (EAGAIN), session hid after the move, crypto_done
+			 * calls, final etype, buffer */
+			int32_t w[8] = { fv[6 * i], fv[6 * i + 1], -2, fv[6 * i + 2], fv[6 * i + 3], fv[6 * i + 4],
+			    fv[6 * i + 5], -2 };
+			int fl;
+			memset(b0, 0, (size_t)rh[i].len);
+			memset(b1, 0, (size_t)rh[i].len);
+			if (rf1[i])
+				w[2] = ffst_result(rf1[i], b0, rh[i].len, &fl);
+			if (rf2[i])
+				w[7] = ffst_result(rf2[i], b1, rh[i].len, &fl);
+			fwrite(w, 4, 8, out);
+			fwrite(b0, 1, (size_t)rh[i].len, out);
+			fwrite(b1, 1, (size_t)rh[i].len, out);
+			if (rf1[i])
+				ffst_free(rf1[i]);
+			if (rf2[i])
+				ffst_free(rf2[i]);
+		}
 		free(b0);
 		free(b1);
 		if (rdef[i])

@@ -4,7 +4,10 @@
  * ESPGPU_ERESTART; fake_poll() completes the staged ones with an etype the
  * request carries in the first ICV byte (0xBA -> ESPGPU_EBADMSG,
  * 0xE1 -> ESPGPU_EINVAL), then unblocks, exactly as ff_gpucrypto_poll does.
- * Probe is the real espgpu_probesession (device-free). */
+ * Probe is the real espgpu_probesession (device-free).
+ * fake_gpu_fail() plays a GPU failure as the engine reports it (espgpu_health):
+ * the staged requests complete with ESPGPU_EIO at the next fake_poll, process()
+ * answers ESPGPU_EIO, probe and newsession ENXIO. */
 #include <stdint.h>
 #include <string.h>
 
@@ -16,17 +19,30 @@ void ff_gpucrypto_done(void *opaque, int abi_etype);
 void ff_gpucrypto_unblock(void);
 
 static struct { void *opaque; int etype; } staged[FAKE_CAP];
-static int nstaged, next_sid;
+static int nstaged, next_sid, failed;
 int fake_freed_sid = -1, fake_last_nsegs;
+
+void fake_gpu_fail(void)
+{
+	failed = 1;
+	for (int i = 0; i < nstaged; i++)
+		staged[i].etype = ESPGPU_EIO;
+}
+
+int ff_gpucrypto_host_failed(void) { return failed; }
 
 int ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
 {
+	if (failed)
+		return ESPGPU_ENXIO;
 	return espgpu_probesession(csp);
 }
 
 int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid)
 {
 	(void)csp;
+	if (failed)
+		return ESPGPU_ENXIO;
 	*sid = next_sid++;
 	return next_sid > 3 ? ESPGPU_ENOMEM : ESPGPU_OK;     /* a 3-slot SA table */
 }
@@ -48,6 +64,8 @@ int ff_gpucrypto_host_process(const struct espgpu_req *r, int hint)
 	uint8_t tag;
 
 	(void)hint;
+	if (failed)
+		return ESPGPU_EIO;
 	if (nstaged == FAKE_CAP)
 		return ESPGPU_ERESTART;
 	fake_last_nsegs = r->nsegs;

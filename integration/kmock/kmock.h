@@ -12,6 +12,12 @@
  *     request on the queue and marks the driver blocked   crypto.c:1413-1460
  *   crypto_unblock clears the block, the queue is retried crypto.c:1191-1210
  *   crypto_done runs the callback (CBIFSYNC: inline)      crypto.c:1802-1830
+ *   crypto_newsession picks the driver whose probe bids best (hardware -100
+ *     over software -500; a positive errno declines)      crypto.c:622-659, 910
+ * With kmock_soft_enable(1) a software driver stand-in (cryptosoft's part:
+ * probe -500 for everything, process completes the request with etype 0 and
+ * leaves the data as is) sits beside the driver under test, so the GPU-failure
+ * path's session migration can be followed (ff_gpucrypto.c gpucrypto_migrate).
  * Inside F-Stack the driver is built against the real headers instead.
  */
 #ifndef KMOCK_H
@@ -119,10 +125,14 @@ struct cryptop {
 #define CRYPTODEV_PROBE_SOFTWARE (-500)
 
 void   *crypto_get_driver_session(crypto_session_t cses);
+const struct crypto_session_params *crypto_get_params(crypto_session_t cses);
+uint32_t crypto_ses2hid(crypto_session_t cses);
 int32_t crypto_get_driverid(device_t dev, size_t session_size, int flags);
 int     crypto_unregister_all(uint32_t driverid);
 int     crypto_unblock(uint32_t driverid, int what);
 void    crypto_done(struct cryptop *crp);
+int     crypto_newsession(crypto_session_t *cses, const struct crypto_session_params *csp, int crid);
+void    crypto_freesession(crypto_session_t cses);
 
 /* The driver's method table (what DEVMETHOD/kobj provide in the kernel). */
 struct kmock_cryptodev {
@@ -145,6 +155,9 @@ struct kmock_stats {
 	int     queued;               /* requests waiting on the crypto queue     */
 	int     done;                 /* crypto_done calls                        */
 	int     unblocks;
+	int     soft_sessions;        /* sessions on the software stand-in        */
+	int     soft_done;            /* requests it completed                    */
+	int     sessions;             /* sessions alive (either driver)           */
 };
 int  kmock_attach(const struct kmock_cryptodev *drv);
 void kmock_detach(void);
@@ -156,5 +169,9 @@ int  kmock_dispatch(struct cryptop *crp);
 /* crypto_proc's pass over the queue after an unblock: re-dispatch in order */
 int  kmock_run_queue(void);
 const struct kmock_stats *kmock_stats(void);
+/* the software driver stand-in beside the driver under test (off: only it) */
+void kmock_soft_enable(int on);
+/* crypto_ses2hid of a session on the software stand-in */
+#define KMOCK_SOFT_ID 8
 
 #endif /* KMOCK_H */

@@ -12,12 +12,20 @@
 extern const struct kmock_cryptodev ff_gpucrypto_kmock;
 int gpucrypto_errno(int abi);
 int fake_poll(void);
+void fake_gpu_fail(void);
 extern int fake_freed_sid, fake_last_nsegs;
 
 #define CHECK(c) do { if (!(c)) { printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); exit(1); } } while (0)
 
 static int ncb;
-static int cb(struct cryptop *crp) { (void)crp; ncb++; return 0; }
+static int ndone[8];           /* crypto_done callbacks per request slot (crp_opaque) */
+static int cb(struct cryptop *crp)
+{
+	ncb++;
+	if (crp->crp_opaque)
+		(*(int *)crp->crp_opaque)++;
+	return 0;
+}
 
 static uint8_t bufs[8][96];
 
@@ -50,6 +58,7 @@ int main(void)
 
 	/* ABI -> FreeBSD errno */
 	CHECK(gpucrypto_errno(ESPGPU_OK) == 0);
+	CHECK(gpucrypto_errno(ESPGPU_EIO) == 5);
 	CHECK(gpucrypto_errno(ESPGPU_EBADMSG) == 89);
 	CHECK(gpucrypto_errno(ESPGPU_ERESTART) == -1);
 	CHECK(gpucrypto_errno(ESPGPU_EAGAIN) == 35);
@@ -129,6 +138,47 @@ int main(void)
 		CHECK(kmock_dispatch(&crp[7]) == 0 && crp[7].crp_etype == EINVAL);
 	}
 
+	/* GPU failure: three requests staged, then the GPU
+	 * fails.  The staged ones complete exactly once with EIO (a clean drop);
+	 * the next request on the session moves it to the software driver
+	 * (EAGAIN with a new session in crp_session, as crypto_invoke's
+	 * CRYPTOCAP_F_CLEANUP branch does) and, re-dispatched as esp_input_cb
+	 * does, completes there; new sessions go to the software driver. */
+	{
+		crypto_session_t s5;
+		const int done0 = st->done;
+
+		kmock_soft_enable(1);
+		memset(ndone, 0, sizeof(ndone));
+		for (int i = 0; i < 3; i++) {
+			esp_gcm_crp(&crp[i], ses, i, 0x00);
+			crp[i].crp_opaque = &ndone[i];
+			CHECK(kmock_dispatch(&crp[i]) == 0);
+		}
+		CHECK(st->done == done0);
+		fake_gpu_fail();
+		esp_gcm_crp(&crp[3], ses, 3, 0x00);
+		crp[3].crp_opaque = &ndone[3];
+		CHECK(kmock_dispatch(&crp[3]) == 0);
+		CHECK(ndone[3] == 1 && crp[3].crp_etype == EAGAIN);
+		CHECK(crp[3].crp_session != ses && crypto_ses2hid(crp[3].crp_session) == KMOCK_SOFT_ID);
+		CHECK(st->soft_sessions == 1);
+		CHECK(kmock_dispatch(&crp[3]) == 0);              /* esp_input_cb's re-dispatch */
+		CHECK(ndone[3] == 2 && crp[3].crp_etype == 0 && st->soft_done == 1);
+		CHECK(fake_poll() == 3);
+		for (int i = 0; i < 3; i++)
+			CHECK(ndone[i] == 1 && crp[i].crp_etype == EIO);
+		CHECK(fake_poll() == 0);
+		for (int i = 0; i < 3; i++)
+			CHECK(ndone[i] == 1);                          /* exactly once */
+		/* the probe declines now: a new session lands on the software driver */
+		CHECK(kmock_newsession(&s5, &csp) == 0 && crypto_ses2hid(s5) == KMOCK_SOFT_ID);
+		CHECK(st->soft_sessions == 2);
+		kmock_freesession(s5);
+		kmock_freesession(crp[3].crp_session);
+		CHECK(st->soft_sessions == 0);
+	}
+
 	kmock_freesession(s3);
 	CHECK(fake_freed_sid == 1);
 	kmock_freesession(ses);
@@ -136,6 +186,7 @@ int main(void)
 	kmock_freesession(s4);
 	kmock_detach();
 	CHECK(st->driverid == -1);
+	CHECK(st->sessions == 0);                 /* every session freed */
 	printf("kmock cpu OK\n");
 	return 0;
 }

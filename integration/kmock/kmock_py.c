@@ -31,6 +31,8 @@ void ff_gpucrypto_host_set_noqueue(int on);
 void ff_gpucrypto_host_fini(void);
 int  ff_gpucrypto_host_register(void *base, uint64_t len);
 int  ff_gpucrypto_host_stats(struct espgpu_stats *st);
+int  ff_gpucrypto_host_tune(const char *key, int value);
+int  ff_gpucrypto_host_failed(void);
 int  ff_gpucrypto_poll(void);
 
 #define KD_MAX_SEGS 16
@@ -39,13 +41,13 @@ struct kd_req {
 	struct cryptop crp;
 	struct mbuf    m[KD_MAX_SEGS];
 	uint8_t        aad[16];
-	int            done;               /* crp_callback ran (crypto_done) */
+	int            done;               /* crp_callback runs (crypto_done calls) */
 };
 
 static int
 kd_cb(struct cryptop *crp)
 {
-	((struct kd_req *)crp)->done = 1;  /* crp is the first member */
+	((struct kd_req *)crp)->done++;    /* crp is the first member */
 	return (0);
 }
 
@@ -215,15 +217,80 @@ kd_counters(int *out4)
 	out4[3] = st->done;
 }
 
-/* engine counters: zero-copy records, overflow entries */
+/* engine counters: zero-copy records, overflow entries, doorbell batches,
+ * GPU failures, requests completed or refused with EIO because of one */
 void
-kd_engine(uint64_t *out3)
+kd_engine(uint64_t *out5)
 {
 	struct espgpu_stats s;
 
 	memset(&s, 0, sizeof(s));
 	ff_gpucrypto_host_stats(&s);
-	out3[0] = s.zerocopy;
-	out3[1] = s.overflow;
-	out3[2] = s.door;
+	out5[0] = s.zerocopy;
+	out5[1] = s.overflow;
+	out5[2] = s.door;
+	out5[3] = s.gpu_fail;
+	out5[4] = s.fail_eio;
+}
+
+/* the GPU-failure path */
+int
+kd_tune(const char *key, int value)
+{
+	return (ff_gpucrypto_host_tune(key, value));
+}
+
+int
+kd_failed(void)
+{
+	return (ff_gpucrypto_host_failed());
+}
+
+/* crypto_done calls so far for the request (exactly one is the contract) */
+int
+kd_done_count(void *r)
+{
+	return (((struct kd_req *)r)->done);
+}
+
+/* the driver id of the request's session now (gpucrypto_migrate moves it) */
+int
+kd_session_hid(void *r)
+{
+	return ((int)crypto_ses2hid(((struct kd_req *)r)->crp.crp_session));
+}
+
+/* esp_input_cb's EAGAIN path: re-dispatch on the session the request now names */
+int
+kd_redispatch(void *r)
+{
+	struct kd_req *q = r;
+
+	q->crp.crp_flags &= ~CRYPTO_F_DONE;
+	return (kmock_dispatch(&q->crp));
+}
+
+void
+kd_soft_enable(int on)
+{
+	kmock_soft_enable(on);
+}
+
+/* software stand-in and session counters: soft sessions, soft completions,
+ * sessions alive, the driver's own id */
+void
+kd_soft(int *out4)
+{
+	const struct kmock_stats *st = kmock_stats();
+
+	out4[0] = st->soft_sessions;
+	out4[1] = st->soft_done;
+	out4[2] = st->sessions;
+	out4[3] = st->driverid;
+}
+
+void
+kd_freesession_of(void *r)
+{
+	kmock_freesession(((struct kd_req *)r)->crp.crp_session);
 }

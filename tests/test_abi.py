@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     assert len(syms) >= 15
     for s in syms:
         assert hasattr(lib, s), "missing export %s" % s
-    assert lib.espgpu_abi_version() == 4
+    assert lib.espgpu_abi_version() == 5
 
 
 def test_struct_layouts():
@@ -26,6 +26,8 @@ def test_struct_layouts():
     assert L.Req.crp_iv.offset % 1 == 0
     # espgpu_req must match the C layout: check a few offsets against natural alignment
     assert L.Req.segs.offset == 16 and L.Req.crp_aad.offset == 32
+    # struct espgpu_stats: 15 uint64 counters (ABI 5 appended gpu_fail, fail_eio)
+    assert C.sizeof(L.Stats) == 15 * 8 and L.Stats.fail_eio.offset == 14 * 8
 
 
 def _probe(**kw):

@@ -51,8 +51,9 @@ def test_gpus2_weak_scaling_configs_plan_full_batches():
 
 
 def test_gpus_more_than_the_node_has_fails_loudly():
-    # this host has no GPU: a real (not dry) 2-GPU run must refuse, not report 1 GPU
-    p = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    # more GPUs than any node has (this host has none, a GPU node at most 8):
+    # a real (not dry) run must refuse, not report a smaller one
+    p = _run(["--gpus", "64", "--steps", "1", "--warmup", "0"])
     assert p.returncode != 0
     assert not any(ln.startswith("{") for ln in p.stdout.splitlines())
     assert "refusing" in p.stderr

@@ -36,7 +36,7 @@ def test_fstack_ipsec_gpu_kernel_domain_compiles_and_links(tmp_path):
     # the driver's calls into the host domain resolve to the host shim
     assert set(rep["gpu_driver_calls_host"]) == {
         "ff_gpucrypto_host_probe", "ff_gpucrypto_host_newsession", "ff_gpucrypto_host_freesession",
-        "ff_gpucrypto_host_process", "ff_gpucrypto_host_ready"}
+        "ff_gpucrypto_host_process", "ff_gpucrypto_host_ready", "ff_gpucrypto_host_failed"}
     assert "ff_gpucrypto_host.c" in rep["host_compiled"]
     # host files that need DPDK headers are named with the header that blocks them
     assert rep["host_blocked"].get("ff_dpdk_if.c", "").startswith("rte_")

@@ -164,14 +164,41 @@ def workload():
     return _workload()
 
 
-def _run(exe, workload, tmp_path):
+def _run(exe, workload, tmp_path, fail=False):
     sessions, reqs, want = workload
     rq, rs = str(tmp_path / "req.bin"), str(tmp_path / "res.bin")
     FR.pack_requests(rq, sessions, reqs)
-    p = subprocess.run([exe, rq, rs], capture_output=True, text=True, timeout=300)
+    p = subprocess.run([exe, rq, rs] + (["--fail"] if fail else []), capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
     assert "fstack_crypto_run OK" in p.stdout
-    return FR.read_results(rs, [len(r["buf"]) for r in reqs])
+    return FR.read_results(rs, [len(r["buf"]) for r in reqs], fail=fail)
+
+
+BSD_EIO, BSD_EAGAIN = 5, 35
+
+
+def _check_failure(res, workload):
+    """The GPU-failure phase (host_main.c --fail), after
+    the normal run checked by _check: every request the engine held when it
+    failed completed exactly once, with EIO and its buffer untouched; every
+    request after it completed with EAGAIN and a cryptosoft session (the
+    driver's session move, crypto.c:1684-1725's protocol) and, re-dispatched
+    as esp_input_cb does, exactly as cryptosoft's own run of it."""
+    sessions, reqs, want = workload
+    gpu_hid, sw_hid, ses, out = res
+    n = 0
+    for i, (q, r) in enumerate(zip(reqs, out)):
+        if ses[q["ses"]][1] != gpu_hid:
+            continue
+        n += 1
+        assert r["f1_dispatch"] == 0 and r["f1_ndone"] == 1, (i, r["f1_dispatch"], r["f1_ndone"])
+        assert r["f1_etype"] == BSD_EIO, (i, r["f1_etype"])
+        assert r["f1_buf"] == q["buf"], i                               # untouched
+        assert r["f2_etype0"] == BSD_EAGAIN and r["f2_hid"] == sw_hid, (i, r["f2_etype0"], r["f2_hid"])
+        assert r["f2_redispatch"] == 0 and r["f2_ndone"] == 2, (i, r["f2_redispatch"], r["f2_ndone"])
+        assert r["f2_etype"] == r["etype_sw"], (i, r["f2_etype"], r["etype_sw"])
+        assert r["f2_buf"] == r["buf_sw"], i                            # cryptosoft's result
+    assert n == len(reqs)
 
 
 def _check(res, workload):
@@ -224,3 +251,26 @@ def test_fstack_opencrypto_with_gpucrypto_gpu(workload, tmp_path):
     # check, which must show as a failure, not a skip
     assert os.path.exists(exe), "integration/fstack_crypto_run_gpu missing: run __graft_entry__.build() where /root/reference exists"
     _check(_run(exe, workload, tmp_path), workload)
+
+
+def test_fstack_gpu_failure_cpu(built, workload, tmp_path):
+    """The GPU-failure path under F-Stack's crypto.c (CPU executable: the
+    oracle stand-in fails with the requests staged)."""
+    exe = built[0]
+    if not os.path.exists(exe):
+        pytest.skip("needs the F-Stack tree to build integration/fstack_crypto_run_cpu")
+    res = _run(exe, workload, tmp_path, fail=True)
+    _check(res, workload)
+    _check_failure(res, workload)
+
+
+@pytest.mark.gpu
+def test_fstack_gpu_failure_gpu(workload, tmp_path):
+    """The GPU-failure path under F-Stack's crypto.c on the MI355X: the
+    engine's next launch fails (set_tuning "fault" 1) with every request
+    staged; each completes once with EIO, later requests move to cryptosoft."""
+    exe = FR.EXE_GPU
+    assert os.path.exists(exe), "integration/fstack_crypto_run_gpu missing: run __graft_entry__.build() where /root/reference exists"
+    res = _run(exe, workload, tmp_path, fail=True)
+    _check(res, workload)
+    _check_failure(res, workload)

@@ -815,3 +815,64 @@ def test_packed_output_rejects(drv):
                                              out.data_ptr(), 1536, 0, None) == 95
     finally:
         drv.freesession(sid)
+
+
+def test_gpu_failure_batch_and_driver_path():
+    """The GPU-failure path on the engine directly (its own context, the
+    module's stays healthy): a device-resident batch whose launch fails
+    (set_tuning "fault" 1) returns EIO and fails the context; every later
+    batch, newsession, process, flush and drain answers EIO (never
+    ERESTART), a request the Python framework dispatches completes at once
+    with EIO, espgpu_health and the stats say so, and close does not hang.
+    A healthy batch before the fault decrypts as the oracle does."""
+    from espgpu.batch import decrypt_batch, descs_to_tensor
+    from espgpu.esp import esp_input_crp
+    from espgpu.opencrypto import CryptoFramework, GpuCryptoDriver
+    d = GpuCryptoDriver(max_sessions=8, batch_records=64, nbatches=2)
+    try:
+        fw = CryptoFramework(d)
+        rng = np.random.default_rng(4800)
+        sa = GcmSA(rng, 16)
+        err, cs = fw.crypto_newsession(sa.esp_sa().csp())
+        assert err == 0 and cs.sid == 0
+        n = 512
+        plain, ct, descs, _ = build_records(rng, [sa], np.zeros(n, dtype=np.int64),
+                                            rng.integers(1, 92, n) * 16)
+        ref = ct.copy()
+        _, ref_st = O.batch([sa.oracle], ref, descs["off4"], descs["len"], descs["sa"])
+        dev = torch.device("cuda:0")
+        arena = torch.from_numpy(np.concatenate([ct, np.zeros(64, np.uint8)])).to(dev)
+        desc = descs_to_tensor(descs, dev)
+        status = torch.zeros(n, dtype=torch.uint8, device=dev)
+        decrypt_batch(d, arena, desc, n, status)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == ref_st).all()
+        m = payload_mask(descs, len(ct))
+        assert (arena.cpu().numpy()[:len(ct)][m] == ref[m]).all()
+        assert d.health() == 0
+        assert d.set_tuning("fault", 8) == O.EINVAL            # unknown bit
+        assert d.set_tuning("fault", 1) == 0
+        arena.copy_(torch.from_numpy(np.concatenate([ct, np.zeros(64, np.uint8)])).to(dev))
+        with pytest.raises(RuntimeError):
+            decrypt_batch(d, arena, desc, n, status)
+        EIO = 5
+        assert d.health() == EIO and "GPU failure" in d.last_error()
+        assert d.lib.espgpu_decrypt_batch(d.ctx, arena.data_ptr(), desc.data_ptr(), n, status.data_ptr(),
+                                          None, 0, None) == EIO
+        assert d.newsession(sa.esp_sa().csp())[0] == EIO
+        pkt = bytearray(bytes(20)) + bytearray(ct[int(descs["off4"][0]) * 4:][:int(descs["len"][0])].tobytes())
+        before = bytes(pkt)
+        crp = esp_input_crp(fw, cs, sa.esp_sa(), pkt, 20)
+        seen = []
+        crp.crp_callback = lambda c: seen.append(c.crp_etype)
+        assert fw.crypto_dispatch(crp) == 0
+        assert seen == [EIO] and bytes(pkt) == before          # completed at once, untouched
+        assert d.flush() == EIO and d.drain() == EIO
+        fw.crypto_poll()
+        assert seen == [EIO]                                   # once
+        st = d.stats()
+        assert st["gpu_fail"] == 1 and st["fail_eio"] == 1
+        assert d.set_tuning("deadline_ms", 0) == O.EINVAL
+        fw.crypto_freesession(cs)                              # host bookkeeping only
+    finally:
+        d.close()

@@ -59,3 +59,18 @@ def test_quad_bitsliced_aes_selftest(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]
     assert r.stdout.startswith("OK")
+
+
+def test_overflow_fifo_arena_selftest(tmp_path):
+    """The host overflow's allocator (fifo_arena.h: a bip buffer of
+    variable-length allocations, freed oldest first): 200 random alloc / pop
+    / undo sequences with wraps against a reference model -- allocations in
+    bounds and disjoint, refused exactly when no placement a bip buffer may
+    use has room, an emptied arena whole again (tools/fifo_selftest.cpp)."""
+    exe = tmp_path / "fifo_selftest"
+    csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
+                    os.path.join(ROOT, "tools", "fifo_selftest.cpp")], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert r.stdout.startswith("OK")

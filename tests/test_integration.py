@@ -30,7 +30,12 @@ def test_host_shim_builds_links_and_probes():
     assert "integration probe OK" in r.stdout
 
 
-def test_kernel_driver_errno_and_erestart():
+def test_kernel_driver_errno_erestart_and_gpu_failure():
+    """kmock_cpu_test: the driver over the kmock KPI and the scripted host
+    layer -- attach flags, errno map, ERESTART queueing, and the GPU-failure
+    path: staged requests complete exactly once with EIO, the next request
+    of a session moves it to the software driver (EAGAIN + new session),
+    new sessions go there, every session is freed."""
     _make()
     r = subprocess.run([os.path.join(D, "kmock_cpu_test")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
@@ -45,7 +50,9 @@ def test_kernel_driver_python_harness_builds():
     _make()
     L = ctypes.CDLL(os.path.join(D, "libkmockdrv.so"))
     for s in ("kd_open", "kd_close", "kd_newsession", "kd_freesession", "kd_request", "kd_dispatch",
-              "kd_poll", "kd_result", "kd_free", "kd_register", "kd_counters", "kd_engine"):
+              "kd_poll", "kd_result", "kd_free", "kd_register", "kd_counters", "kd_engine",
+              "kd_tune", "kd_failed", "kd_done_count", "kd_session_hid", "kd_redispatch", "kd_soft_enable",
+              "kd_soft", "kd_freesession_of"):
         assert hasattr(L, s), s
 
 

@@ -136,9 +136,9 @@ class KmockDriver:
         return dict(zip(("erestarts", "queued", "blocked", "done"), list(a)))
 
     def engine(self):
-        a = (C.c_uint64 * 3)()
+        a = (C.c_uint64 * 5)()
         self.L.kd_engine(a)
-        return dict(zip(("zerocopy", "overflow", "door"), list(a)))
+        return dict(zip(("zerocopy", "overflow", "door", "gpu_fail", "fail_eio"), list(a)))
 
     def free(self, reqs):
         for r in reqs:
@@ -565,3 +565,114 @@ def _req_view(kd, build, ses, esa, view):
     kd._keep.append((arr, bases, lens))
     assert kd.dispatch(r) == 0
     return r
+
+
+# ---------------------------------------------------------------------------
+# GPU failure: every cryptop completes exactly once
+
+KMOCK_SOFT_ID, BSD_EIO, BSD_EAGAIN = 8, 5, 35
+FAULT_LAUNCH, FAULT_QUERY, FAULT_STUCK = 1, 2, 4     # set_tuning "fault" (include/espgpu.h)
+
+
+@pytest.mark.parametrize("fault,door", [(FAULT_LAUNCH, 0), (FAULT_QUERY, 0), (FAULT_STUCK, 0),
+                                        (FAULT_LAUNCH, 16), (FAULT_STUCK, 16)],
+                         ids=["launch", "query", "stuck", "launch-door", "stuck-door"])
+def test_gpu_failure_completes_every_request_once(fault, door):
+    """F-Stack mode (two 16-record slots and the host overflow), optionally on
+    the doorbell path.  After 16 requests complete normally, a fault is
+    injected (set_tuning "fault": the next launch fails / the next completion
+    query returns an error / the next batch is never seen to complete, which
+    meets deadline_ms) and 80 more requests are dispatched.  Main-loop
+    iterations then complete every one of them exactly once -- crypto_done
+    called once per cryptop, with no hang -- either with the oracle's
+    plaintext (its batch completed) or with EIO and the buffer untouched (a
+    clean drop, esp_input_cb's esps_noxform); the engine counts one failure
+    and as many EIO completions.  Afterwards the next request of the session
+    completes with EAGAIN and a session on the software driver, and its
+    re-dispatch (esp_input_cb's EAGAIN path) completes there; a new session
+    goes to the software driver (the probe declines)."""
+    from espgpu.esp import esp_input_crp
+    kd = KmockDriver(batch_records=16, nbatches=2, noqueue=True)
+    L = kd.L
+    L.kd_tune.argtypes = [C.c_char_p, C.c_int]
+    for f in ("kd_done_count", "kd_session_hid", "kd_redispatch", "kd_freesession_of"):
+        getattr(L, f).argtypes = [C.c_void_p]
+    try:
+        if door:
+            assert L.kd_tune(b"door", door) == 0
+        rng = np.random.default_rng(4700 + fault + door)
+        sa = GcmSA(rng, 16)
+        n = 96
+        cts = rng.integers(1, 92, n) * 16
+        plain, ct, descs, eh = build_records(rng, [sa], np.zeros(n, dtype=np.int64), cts)
+        ref = ct.copy()
+        _, ref_st = O.batch([sa.oracle], ref, descs["off4"], descs["len"], descs["sa"])
+        assert (ref_st == 0).all()
+        esa = sa.esp_sa()
+        e, ses = kd.newsession(esa)
+        assert e == 0
+
+        def mk(i):
+            bufs = bytearray(_pkt(ct, descs, i))
+            return kd.request(ses, esp_input_crp(_Fw(), ses, esa, bufs, 20), bufs), bufs
+
+        def check_pt(i, bufs):
+            o, Ln = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            assert bytes(bufs[20 + 16:20 + Ln - 16]) == ref[o + 16:o + Ln - 16].tobytes(), i
+
+        warm = [mk(i) for i in range(16)]
+        for r, _ in warm:
+            assert kd.dispatch(r) == 0
+        assert kd.wait([r for r, _ in warm]) == [0] * 16
+        for i, (_, b) in enumerate(warm):
+            check_pt(i, b)
+        assert L.kd_failed() == 0
+        if fault == FAULT_STUCK:
+            assert L.kd_tune(b"deadline_ms", 200) == 0
+        assert L.kd_tune(b"fault", fault) == 0
+        reqs = [mk(i) for i in range(16, n)]
+        for r, _ in reqs:
+            assert kd.dispatch(r) == 0
+        t0 = time.monotonic()
+        ets = kd.wait([r for r, _ in reqs], timeout_s=30.0)
+        assert time.monotonic() - t0 < 10.0
+        assert L.kd_failed() == 1
+        for _ in range(64):                              # more main-loop iterations deliver nothing twice
+            L.kd_poll()
+        assert [L.kd_done_count(r) for r, _ in reqs] == [1] * len(reqs)
+        n_eio = 0
+        for k, (et, (r, bufs)) in enumerate(zip(ets, reqs)):
+            i = 16 + k
+            if et == 0:
+                check_pt(i, bufs)
+            else:
+                assert et == BSD_EIO, (i, et)
+                assert bytes(bufs) == _pkt(ct, descs, i), i          # untouched
+                n_eio += 1
+        assert n_eio >= 48 if fault != FAULT_LAUNCH else n_eio == len(reqs)
+        eng = kd.engine()
+        assert eng["gpu_fail"] == 1 and eng["fail_eio"] == n_eio, eng
+        kd.free([r for r, _ in warm + reqs])
+        # after the failure: the session moves to the software driver
+        L.kd_soft_enable(1)
+        r, bufs = mk(0)
+        assert kd.dispatch(r) == 0
+        assert L.kd_done_count(r) == 1 and L.kd_result(r) == BSD_EAGAIN
+        assert L.kd_session_hid(r) == KMOCK_SOFT_ID
+        assert L.kd_redispatch(r) == 0
+        assert L.kd_done_count(r) == 2 and L.kd_result(r) == 0
+        soft = (C.c_int * 4)()
+        L.kd_soft(soft)
+        assert soft[0] == 1 and soft[1] == 1
+        L.kd_freesession_of(r)
+        kd.free([r])
+        e2, ses2 = kd.newsession(esa)                    # the probe declines: software
+        assert e2 == 0
+        L.kd_soft(soft)
+        assert soft[0] == 1
+        kd.freesession(ses2)
+        kd.freesession(ses)
+        L.kd_soft(soft)
+        assert soft[0] == 0 and soft[2] == 0             # every session freed
+    finally:
+        kd.close()                                       # bounded: the failed ctx waits on nothing

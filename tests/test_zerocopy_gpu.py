@@ -685,3 +685,67 @@ def test_door_fstack_loop_with_overflow():
             assert bytes(pkts[i][16:L - 16]) == bytes(plain[o + 16:o + L - 16])
     finally:
         drv.close()
+
+
+def test_door_launched_door_order_does_not_wait_for_idle_timeout():
+    """A door job, then launched work, then another door job before the door
+    kernel has exited (four staging slots, all three in flight at once).  The
+    launched work's retire request must stand while that work is outstanding:
+    cancelling it for the second door job would keep the kernel resident for
+    its 20-ms idle timeout, and launched work behind it on a shared hardware
+    queue would wait that long.  The launched batch completes in far less;
+    every result vs the oracle."""
+    import time
+    from espgpu.opencrypto import CRYPTO_F_DONE, CryptoFramework
+    drv = _driver(max_sessions=16, nbatches=4)
+    try:
+        assert drv.set_tuning("door", 32) == 0              # default door_idle_us: 20 ms
+        fw = CryptoFramework(drv)
+        rng = np.random.default_rng(2760)
+        sa = GcmSA(rng, 16)
+        err, cs = fw.crypto_newsession(sa.esp_sa().csp())
+        assert err == 0
+        sas = _sas(rng)
+        ses = [fw.crypto_newsession(s.esp_sa().csp())[1] for s in sas]
+
+        def burst(n, mixed):
+            idx = rng.integers(0, len(sas), n) if mixed else np.zeros(n, dtype=np.int64)
+            use = sas if mixed else [sa]
+            plain, ct, descs, _ = build_records(rng, use, idx, _cts(rng, use, idx))
+            out = []
+            for i in range(n):
+                o, Ln = int(descs["off4"][i]) * 4, int(descs["len"][i])
+                s_ = use[idx[i]]
+                pkt = bytearray(bytes(ct[o:o + Ln]))
+                crp = esp_input(fw, ses[idx[i]] if mixed else cs, s_.esp_sa(), pkt, 0, 0)
+                out.append((crp, pkt, bytes(plain[o + s_.hlen:o + Ln - s_.mlen]), s_))
+            return out
+
+        d0 = drv.stats()["door"]
+        worst = 0.0
+        for rnd in range(5):
+            A, B, C_ = burst(32, False), burst(40, True), burst(32, False)
+            for grp in (A, B, C_):
+                for crp, *_ in grp:
+                    assert fw.crypto_dispatch(crp) == 0
+                fw.crypto_flush()
+                if grp is B:
+                    t0 = time.perf_counter()
+            while not all(crp.crp_flags & CRYPTO_F_DONE for crp, *_ in B):
+                fw.crypto_poll()
+                assert time.perf_counter() - t0 < 2.0
+            tb = time.perf_counter() - t0
+            fw.crypto_drain()
+            if rnd:                                            # round 0 allocates the planner workspace
+                worst = max(worst, tb)
+            for grp in (A, B, C_):
+                for crp, pkt, pt, s_ in grp:
+                    assert crp.crp_etype == 0
+                    assert bytes(pkt[s_.hlen:len(pkt) - s_.mlen]) == pt
+        assert worst < 0.010, worst                            # << the 20-ms idle timeout
+        assert drv.stats()["door"] - d0 == 10
+        for s_ in ses:
+            fw.crypto_freesession(s_)
+        fw.crypto_freesession(cs)
+    finally:
+        drv.close()
