@@ -125,8 +125,9 @@ def read_results(path, lens, fail=False):
     """-> (gpu_hid, sw_hid, sessions [(err_def, hid_def, err_sw, hid_sw)],
     requests [dict etype, done_flag, buf, etype_sw, done_flag_sw, buf_sw,
     dispatch, dispatch_sw]; with fail (host_main.c --fail) also f1_dispatch,
-    f1_ndone, f1_etype, f1_buf (held when the GPU failed), f2_redispatch,
-    f2_etype0, f2_hid, f2_ndone, f2_etype, f2_buf (dispatched after it)]"""
+    f1_ndone0, f1_etype0, f1_ndone, f1_etype, f1_buf (dispatched as the GPU
+    failed: held, or refused and moved), f2_redispatch, f2_etype0, f2_hid,
+    f2_ndone, f2_etype, f2_buf (dispatched after it)]"""
     with open(path, "rb") as f:
         magic, nses, nreq, gh, sh = struct.unpack("<IIIii", f.read(20))
         assert magic == 0x53525346 and nreq == len(lens)
@@ -138,9 +139,10 @@ def read_results(path, lens, fail=False):
             d = dict(etype=v[0], done_flag=v[1], buf=b0, etype_sw=v[2], done_flag_sw=v[3], buf_sw=b1,
                      dispatch=v[4], dispatch_sw=v[5])
             if fail:
-                w = struct.unpack("<8i", f.read(32))
-                d.update(f1_dispatch=w[0], f1_ndone=w[1], f1_etype=w[2], f2_redispatch=w[3], f2_etype0=w[4],
-                         f2_hid=w[5], f2_ndone=w[6], f2_etype=w[7], f1_buf=f.read(n), f2_buf=f.read(n))
+                w = struct.unpack("<10i", f.read(40))
+                d.update(f1_dispatch=w[0], f1_ndone0=w[1], f1_etype0=w[2], f1_ndone=w[3], f1_etype=w[4],
+                         f2_redispatch=w[5], f2_etype0=w[6], f2_hid=w[7], f2_ndone=w[8], f2_etype=w[9],
+                         f1_buf=f.read(n), f2_buf=f.read(n))
             reqs.append(d)
     return gh, sh, ses, reqs
 

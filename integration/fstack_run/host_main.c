@@ -186,7 +186,7 @@ main(int argc, char **argv)
 	/* 5. the GPU-failure phase: f1 = the requests the engine holds when it
 	 * fails, f2 = requests after it */
 	void **rf1 = calloc(nreq, sizeof(void *)), **rf2 = calloc(nreq, sizeof(void *));
-	int32_t *fv = calloc(6 * (size_t)nreq, sizeof(int32_t));
+	int32_t *fv = calloc(8 * (size_t)nreq, sizeof(int32_t));
 	if (fail) {
 #ifdef FSR_GPU
 		if (ff_gpucrypto_host_tune("fault", 1) != 0)
@@ -199,7 +199,7 @@ main(int argc, char **argv)
 			    rh[i].len, rh[i].cuts, rh[i].ncuts);
 			if (rf1[i] == NULL)
 				die("request");
-			fv[6 * i] = ffst_dispatch(rf1[i]);
+			fv[8 * i] = ffst_dispatch(rf1[i]);
 		}
 #ifndef FSR_GPU
 		oracle_engine_fail();
@@ -221,17 +221,25 @@ main(int argc, char **argv)
 		if (!ff_gpucrypto_host_failed())
 			die("the engine does not report the failure");
 		for (uint32_t i = 0; i < nreq; i++) {
+			int hid;
 			if (rf1[i] == NULL)
 				continue;
-			fv[6 * i + 1] = ffst_ndone(rf1[i]);
+			/* a request dispatched as the engine failed (the one whose staging
+			 * found the slot full and the launch failing) was refused, not
+			 * held: it completed with EAGAIN on a cryptosoft session, and
+			 * esp_input_cb re-dispatches it */
+			fv[8 * i + 1] = ffst_ndone(rf1[i]);
+			if (ffst_redispatch(rf1[i], &fv[8 * i + 2], &hid) != -1 && hid != sw_hid)
+				die("moved to a session not on cryptosoft");
+			fv[8 * i + 3] = ffst_ndone(rf1[i]);
 			rf2[i] = ffst_request(sdef[rh[i].ses], rh[i].f, rh[i].aad, rh[i].esn, rh[i].iv, bufs[i],
 			    rh[i].len, rh[i].cuts, rh[i].ncuts);
 			if (rf2[i] == NULL)
 				die("request");
 			if (ffst_dispatch(rf2[i]) != 0)                /* completes at once (EAGAIN) */
 				die("dispatch after the failure");
-			fv[6 * i + 2] = ffst_redispatch(rf2[i], &fv[6 * i + 3], &fv[6 * i + 4]);
-			fv[6 * i + 5] = ffst_ndone(rf2[i]);
+			fv[8 * i + 4] = ffst_redispatch(rf2[i], &fv[8 * i + 5], &fv[8 * i + 6]);
+			fv[8 * i + 7] = ffst_ndone(rf2[i]);
 		}
 	}
 
@@ -256,19 +264,20 @@ main(int argc, char **argv)
 		fwrite(b0, 1, (size_t)rh[i].len, out);
 		fwrite(b1, 1, (size_t)rh[i].len, out);
 		if (fail) {
-			/* f1: dispatch, crypto_done calls, etype, buffer; f2: redispatch rc,
-			 * etype before it (EAGAIN), session hid after the move, crypto_done
+			/* f1: dispatch, crypto_done calls when the poll had run, the first
+			 * etype, crypto_done calls in all, final etype, buffer; f2: redispatch
+			 * rc, etype before it (EAGAIN), session hid after the move, crypto_done
 			 * calls, final etype, buffer */
-			int32_t w[8] = { fv[6 * i], fv[6 * i + 1], -2, fv[6 * i + 2], fv[6 * i + 3], fv[6 * i + 4],
-			    fv[6 * i + 5], -2 };
+			int32_t w[10] = { fv[8 * i], fv[8 * i + 1], fv[8 * i + 2], fv[8 * i + 3], -2, fv[8 * i + 4],
+			    fv[8 * i + 5], fv[8 * i + 6], fv[8 * i + 7], -2 };
 			int fl;
 			memset(b0, 0, (size_t)rh[i].len);
 			memset(b1, 0, (size_t)rh[i].len);
 			if (rf1[i])
-				w[2] = ffst_result(rf1[i], b0, rh[i].len, &fl);
+				w[4] = ffst_result(rf1[i], b0, rh[i].len, &fl);
 			if (rf2[i])
-				w[7] = ffst_result(rf2[i], b1, rh[i].len, &fl);
-			fwrite(w, 4, 8, out);
+				w[9] = ffst_result(rf2[i], b1, rh[i].len, &fl);
+			fwrite(w, 4, 10, out);
 			fwrite(b0, 1, (size_t)rh[i].len, out);
 			fwrite(b1, 1, (size_t)rh[i].len, out);
 			if (rf1[i])
