@@ -23,11 +23,8 @@
 //    the quad's four records, a DPP transpose hands each lane its own), two
 //    64-byte blocks per load.
 //  * Decrypt is verify-first: an HMAC pass (lane = record), then a
-//    block-parallel decrypt of the verified records (MODE 3 out of place, the
-//    default and benchmarked path; MODE 2 in place).  MODE 0 (set_tuning
-//    eta_fused = 1) is the one-pass alternative: every 64-byte HMAC chunk the
-//    lane loads also completes up to four cipher blocks, which it decrypts
-//    with four AES states in flight and stores, so the record is read once.
+//    block-parallel decrypt of the verified records (MODE 3 out of place;
+//    MODE 2 in place, the opencrypto contract).
 //  * In-place verify-first decrypt (MODE 2) must authenticate before it may
 //    overwrite: HMAC pass first, then a block-parallel pass -- the wave walks
 //    its records as one flat block list, 64 consecutive blocks per pass
@@ -55,84 +52,24 @@ namespace {
 constexpr uint32_t LDS_T = 0;          // Td0/Td1 (decrypt) or Te0/Te1 (encrypt), 64 KiB
 constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32 KiB
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
-constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 || mode == 6 ? 65536u : 163840u; }
+constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 ? 65536u : 163840u; }
 
-#ifndef ETA_PROBE_SHA1ONLY
-#define ETA_PROBE_SHA1ONLY 0 // measurement probe: MODE 2/3 narrow launches without SHA2-256 code (wrong for SHA-256 SAs)
-#endif
-#ifndef ETA_ENC_QUAD
-#define ETA_ENC_QUAD 1       // encrypt MAC pass (MODE 1): SHA-1 / SHA2-256 ICVs with hmac_quad
-#endif
-#ifndef ETA_ENC_QUAD4
-#define ETA_ENC_QUAD4 1      // MODE 4 CBC: cbc_enc_quad (quad-coalesced 64-byte groups)
-#endif
-#ifndef ETA_WG1
-#define ETA_WG1 1024         // encrypt MAC pass (MODE 1) for SHA-1 / SHA2-256 / no-auth sessions
-#endif
-#ifndef ETA_HQ_NB1
-#define ETA_HQ_NB1 2         // MAC pass (MODE 1): hmac_quad blocks per load
-#endif
-#ifndef ETA_HQ_NB2
-#define ETA_HQ_NB2 2         // in-place verify (MODE 2): hmac_quad blocks per load
-#endif
-#ifndef ETA_ENC_NB
-#define ETA_ENC_NB 1         // cbc_enc_quad: 64-byte groups per load / store
-#endif
-#ifndef ETA_ENC_WPE
-#define ETA_ENC_WPE 8        // MODE 4 CBC: minimum waves per SIMD (8: <= 64 VGPRs, two workgroups per CU)
-#endif
-#ifndef ETA_STAGGER
-#define ETA_STAGGER 0        // probe: delay (s_memrealtime ticks) of the late-starting waves
-#endif
-#ifndef ETA_STAGGER_MODE
-#define ETA_STAGGER_MODE 0   // 0: odd waves start late; 1: wave w starts (w & 3) delays late
-#endif
-#ifndef ETA_XCDQ
-#define ETA_XCDQ 0           // per-XCD work-queue tickets (xcd_ticket)
-#endif
-#ifndef ETA_HMAC_QUAD
-#define ETA_HMAC_QUAD 1      // MODE 2 verify with quad-coalesced block loads (hmac_quad); 0: hmac_t
-#endif
-#ifndef ETA_U
-#define ETA_U 4              // blocks per lane per pass of the block-parallel decrypt
-#endif
-#ifndef ETA_WG2
-#define ETA_WG2 1024         // in-place verify-first launch (MODE 2, SHA-1 / SHA2-256 sessions; 128 VGPRs with hmac_quad)
-#endif
-#ifndef ETA_WG3
-#define ETA_WG3 768
-#endif
-#ifndef ETA_HMAC_PAIR
-#define ETA_HMAC_PAIR 0
-#endif
-#ifndef ETA_HMAC_PREFETCH
-#define ETA_HMAC_PREFETCH 0
-#endif
-#ifndef ETA_LEAN_SHFL
-#define ETA_LEAN_SHFL 1
-#endif
-#ifndef ETA_LANE_MAP
-#define ETA_LANE_MAP 0
-#endif
-
-
-constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds
-// MODE 2 / 3 session sets (the CKS template argument): every ETA session, or
-// split by hash so that the common kernel carries no SHA-512 code (its
-// registers then fit without spilling): HMAC-SHA1 / SHA2-256 / none, or
-// HMAC-SHA2-384 / 512 only
-[[maybe_unused]] constexpr int CK_ALL = -1;                     // variants build only
+constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds (MODE 4)
+// MODE 1 / 2 / 3 session sets (the CKS template argument), split by hash so
+// that the common kernel carries no SHA-512 code (its registers then fit
+// without spilling): HMAC-SHA1 / SHA2-256 / none, or HMAC-SHA2-384 / 512 only
 constexpr int CK_NARROW = -2, CK_WIDEH = -3;
+constexpr int kEtaU = 4;               // blocks per lane per pass of the block-parallel decrypt
 constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
 
 typedef const __attribute__((address_space(4))) uint32_t *kptr;
 
-// Measurement knobs for the fused decrypt (MODE 0), compiled in only by
-// `make knobs` (bench.py --tuning eta_opts=N with ESPGPU_LIB pointing at
-// libespgpu_knobs.so): bit0 folds every record into the first 1 MiB of the
-// arena (L2-resident loads and stores), bit1 skips the AES rounds, bit2 the
-// HMAC compressions, bit3 the full chunks' plaintext stores.  They break
-// results on purpose, to split the kernel's time.
+// Measurement knobs for the decrypt kernels, compiled in only by `make knobs`
+// (bench.py --tuning eta_opts=N with ESPGPU_LIB pointing at
+// libespgpu_knobs.so): 0x10000 skips the verify pass (every record decrypts),
+// 0x20000 the HMAC compressions (the loads stay), 0x40000 the decrypt pass's
+// AES, 0x80000 its loads and stores.  They break results on purpose, to split
+// the kernel's time.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t e_opts;
 __device__ __forceinline__ uint32_t eopts() {
@@ -509,57 +446,17 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
 #pragma unroll
   for (int k = 0; k < 8; ++k) h[k] = k < W ? ipad[k] : 0u;
   uint32_t w[16];
-#if ETA_HMAC_PREFETCH
-  // the next full block's 64 bytes are loaded while this one is compressed
-  uint4 nx[4];
-  if (nfull > 0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nx[q] = ld16(rec + 16 * q);
-  }
-#endif
-#if ETA_HMAC_PAIR
-  // full blocks two at a time: the 128 bytes are loaded together, so every
-  // cache line of the record is consumed within one step
-  uint32_t b = 0;
-  for (; b + 1 < nfull; b += 2) {
-    uint4 q8[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) q8[q] = ld16(rec + 64 * b + 16 * q);
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = bswap4(q8[4 * half + q]);
-        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-      }
-      Hash<HS>::compress(h, w);
-    }
-  }
-  for (; b <= total; ++b) {
-#else
   // One compression site for every block (inner data, inner padding, outer)
-  // keeps a single inlined copy of the rounds.
+  // keeps a single inlined copy of the rounds.  (Prefetching the next block,
+  // or two blocks per step, measured equal or slower: DESIGN.md §6.)
   for (uint32_t b = 0; b <= total; ++b) {
-#endif
     if (b < nfull) {
-#if ETA_HMAC_PREFETCH
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = bswap4(nx[q]);
-        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-      }
-      if (b + 1 < nfull) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nx[q] = ld16(rec + 64 * (b + 1) + 16 * q);
-      }
-#else
       const uint8_t *p = rec + 64 * b;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint4 v = bswap4(ld16(p + 16 * q));
         w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
       }
-#endif
     } else if (b < total) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
@@ -579,8 +476,8 @@ __device__ void hmac_t(const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_h
   for (int k = 0; k < 8; ++k) out[k] = h[k];
 }
 
-// hmac_t for a whole wave whose lanes each verify one record (MODE 2 / 3,
-// ETA_HMAC_QUAD): the same hash, but a block's 64 bytes reach their lane by
+// hmac_t for a whole wave whose lanes each verify one record (MODE 2's
+// verify, MODE 1's ICVs): the same hash, but a block's 64 bytes reach their lane by
 // a coalesced load.  Lane 4Q+k loads piece k (16 bytes) of block b of each of
 // the quad's 4 records, so one load instruction covers 16 records x 64
 // contiguous bytes (16 lines) instead of 64 records x 16 bytes (64 lines), and
@@ -787,33 +684,6 @@ __device__ void cbc_enc_quad(bool act, uint8_t *rec, uint32_t nb0, kptr ek, int 
   }
 }
 
-// One block of hmac_t's loop (block b of the inner message, its padding, or
-// b == total: the outer block from the opad state), for callers that
-// interleave the hash with other work (MODE 7).
-template <int HS>
-__device__ __forceinline__ void hmac_step(uint32_t h[8], const uint8_t *rec, uint32_t b, uint32_t nfull,
-                                          uint32_t total, uint32_t L0, uint32_t L, bool esn, uint32_t esn_hi,
-                                          uint64_t bits, kptr opad) {
-  constexpr int W = Hash<HS>::W;
-  uint32_t w[16];
-  if (b < nfull) {
-    const uint8_t *q = rec + 64 * b;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 v = bswap4(ld16(q + 16 * k));
-      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-    }
-  } else if (b < total) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
-  } else {
-    outer_block<HS>(h, w);
-#pragma unroll
-    for (int k = 0; k < W; ++k) h[k] = opad[k];
-  }
-  Hash<HS>::compress(h, w);
-}
-
 // ---- SHA-512 / SHA-384 compression (SHA512_Transform, freebsd/crypto/sha2/sha512c.c:196) ----
 // 64-bit words held as uint64_t; rotations as two v_alignbit on the halves.
 __constant__ uint64_t kK512[80] = ESPGPU_SHA512_K;
@@ -919,219 +789,8 @@ __device__ void hmac_wide(const uint8_t *rec, uint32_t L0, bool esn, uint32_t es
 __device__ __forceinline__ bool wide_hash(uint32_t aalg) {
   return aalg == ESPGPU_CRYPTO_SHA2_384_HMAC || aalg == ESPGPU_CRYPTO_SHA2_512_HMAC;
 }
-// Sessions only the two-pass kernels (MODE 3 / MODE 2) serve: SHA2-384/512
-// (128-byte hash blocks), no auth (CSP_MODE_CIPHER: aalg 0) and ESP-NULL
-// (the identity cipher).  The one-pass MODE 0 and the split MODE 6 / 5
-// kernels take SHA-1 / SHA2-256 with AES-CBC / AES-CTR only.
-__device__ __forceinline__ bool two_pass_only(uint32_t calg, uint32_t aalg) {
-  return wide_hash(aalg) || aalg == 0 || calg == ESPGPU_CRYPTO_NULL_CBC;
-}
 
 __device__ __forceinline__ kptr kp(const void *p) { return (kptr)p; }
-
-// One pass over an ETA record for the out-of-place decrypt: the record is
-// read once, in 64-byte HMAC chunks (lane = record); each chunk feeds the
-// hash compression AND the decryption of the cipher blocks it completes, so
-// the ciphertext is not fetched a second time for the cipher.
-//  CBC (hlen 24): chunk 0 holds the IV (C_-1) and blocks 0, 1; chunk b >= 1
-//    holds the 8-byte tail of block 4b-2 and blocks 4b-1 .. 4b+1, whose other
-//    8 bytes came at the end of chunk b-1 (carried in two registers).
-//  CTR (hlen 16): chunk 0 holds the IV and blocks 0..2; chunk b >= 1 holds
-//    blocks 4b-1 .. 4b+2.  Keystream = AES_K(nonce || IV || be32(i+1)).
-// The <= 4 blocks after the last full chunk are decrypted on the way through
-// the first partial chunk.  Writes plaintext to out (MODE 0 decrypts records
-// whose ICV fails too; the status byte says so, as in the GCM kernel).
-// Returns whether the first mlen bytes of the HMAC match the ICV; *trl gets
-// the esp_input_cb trailer word from the last block.
-// Per-wave 4 KiB staging tile for the plaintext of the full chunks: (record
-// r of the wave, 16-byte part k) at bank line 4*(r>>4) + k, slot
-// 4*((p+q)&3) + ((k+q)&3) with u = r&15, p = u>>2, q = u&3.  Conflict-free
-// per 16-lane group both for a lane writing its own record's part k and for
-// 4-lane groups reading one record's 64 contiguous bytes.
-__device__ __forceinline__ uint32_t tile_off(int r, int k) {
-  const int u = r & 15, pp = u >> 2, q = u & 3;
-  return (uint32_t)(((r >> 4) * 4 + k) * 256 + (4 * ((pp + q) & 3) + ((k + q) & 3)) * 16);
-}
-
-template <int CK, int HS>
-__device__ __forceinline__ bool eta_decrypt_fused(const uint8_t *rec, uint8_t *orec, uint32_t plen, uint32_t mlen, bool esn,
-                                  uint32_t esn_hi, uint32_t salt, kptr ipad, kptr opad, kptr key, int nr,
-                                  const uint8_t *lds, uint8_t *tile, uint8_t *out, uint32_t off, uint32_t slot,
-                                  bool act, uint32_t *trl) {
-  constexpr int W = Hash<HS>::W;
-  const int lane = threadIdx.x & 63, qb = lane & ~3, pi = lane & 3;
-  constexpr uint32_t HL = CK == CK_CBC ? 24u : 16u;
-  const uint32_t L0 = HL + plen, L = L0 + (esn ? 4u : 0u);
-  const uint32_t nfull = L0 / 64, total = (L + 9 + 63) / 64, nct = (plen + 15) / 16;
-  const uint64_t bits = (uint64_t)(64 + L) * 8;
-  const uint8_t *te = lds + LDS_TE;
-  uint32_t T = act ? total : 0;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) T = max(T, (uint32_t)__shfl_xor((int)T, o));
-  uint32_t h[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) h[k] = k < W ? ipad[k] : 0u;
-  uint4 prev = make_uint4(0, 0, 0, 0);
-  uint32_t cy0 = 0, cy1 = 0;                // CBC carry / CTR explicit IV
-  for (uint32_t b = 0; b <= T; ++b) {
-    const bool on = act && b <= total;
-    uint32_t w[16];
-    const bool full = on && b < nfull;
-    if (full) {
-      uint32_t m[16];
-      const uint8_t *q = rec + 64 * b;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint4 v = ld16(q + 16 * k);
-        m[4 * k] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
-      }
-      if (CK == CK_CBC) {
-        uint4 blk[4];
-        int nb;
-        if (b == 0) {                       // wave-uniform: every lane is at chunk 0 together
-          prev = make_uint4(m[2], m[3], m[4], m[5]);
-          blk[0] = make_uint4(m[6], m[7], m[8], m[9]);
-          blk[1] = make_uint4(m[10], m[11], m[12], m[13]);
-          blk[2] = blk[3] = make_uint4(0, 0, 0, 0);
-          nb = 2;
-        } else {
-          blk[0] = make_uint4(cy0, cy1, m[0], m[1]);
-          blk[1] = make_uint4(m[2], m[3], m[4], m[5]);
-          blk[2] = make_uint4(m[6], m[7], m[8], m[9]);
-          blk[3] = make_uint4(m[10], m[11], m[12], m[13]);
-          nb = 4;
-        }
-        cy0 = m[14];
-        cy1 = m[15];
-        uint4 d[4] = {blk[0], blk[1], blk[2], blk[3]};
-        if (!(eopts() & 2)) aes_dec4(d, key, nr, lds, slot);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (k < nb) {
-            // to the tile; stored below 4 lanes per record
-            *reinterpret_cast<uint4 *>(tile + tile_off(lane, k)) = xor4(d[k], prev);
-            prev = blk[k];
-          }
-        }
-      } else {
-        if (b == 0) {
-          cy0 = m[2];
-          cy1 = m[3];
-        }
-        uint4 ks[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ks[k] = make_uint4(salt, cy0, cy1, bswap32(4 * b + (uint32_t)k));
-        if (!(eopts() & 2)) aes_enc4(ks, key, nr, te, slot);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (b > 0 || k > 0)                                      // chunk 0 starts with SPI|SN|IV
-            *reinterpret_cast<uint4 *>(tile + tile_off(lane, b > 0 ? k : k - 1)) =
-                xor4(make_uint4(m[4 * k], m[4 * k + 1], m[4 * k + 2], m[4 * k + 3]), ks[k]);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = bswap32(m[k]);
-    } else if (on && b < total) {
-      // the hash words first: in place, the stores below overwrite the tail
-#pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = tail_word(rec, b, k, L0, L, esn, esn_hi, total, bits);
-      if (b == nfull) {
-        // the cipher blocks after the last full chunk (1..4 of them)
-        if (CK == CK_CBC) {
-          const int i0 = nfull == 0 ? 0 : 4 * (int)nfull - 2;
-          if (nfull == 0) prev = ld16(rec + 8);
-          uint4 blk[4], d[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            blk[k] = make_uint4(0, 0, 0, 0);
-            if (i0 + k < (int)nct) blk[k] = ld16(rec + HL + 16 * (i0 + k));
-            d[k] = blk[k];
-          }
-          aes_dec4(d, key, nr, lds, slot);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (i0 + k < (int)nct) {
-              const uint4 pt = xor4(d[k], prev);
-              st16(orec + HL + 16 * (i0 + k), pt);
-              if (i0 + k == (int)nct - 1) *trl = esp_trailer_word(pt.w, plen);
-              prev = blk[k];
-            }
-          }
-        } else {
-          const int i0 = nfull == 0 ? 0 : 4 * (int)nfull - 1;
-          if (nfull == 0) {
-            cy0 = *reinterpret_cast<const uint32_t *>(rec + 8);
-            cy1 = *reinterpret_cast<const uint32_t *>(rec + 12);
-          }
-          uint4 c[4], ks[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            c[k] = make_uint4(0, 0, 0, 0);
-            if (i0 + k < (int)nct) c[k] = ld16(rec + HL + 16 * (i0 + k));
-            ks[k] = make_uint4(salt, cy0, cy1, bswap32((uint32_t)(i0 + k) + 1u));
-          }
-          aes_enc4(ks, key, nr, te, slot);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (i0 + k < (int)nct) {
-              const int rem = (int)plen - 16 * (i0 + k);
-              const uint4 pt = xor4(c[k], ks[k]);
-              st_partial(orec + HL + 16 * (i0 + k), pt, rem);
-              if (i0 + k == (int)nct - 1) *trl = esp_trailer_word(last_word(pt, rem), plen);
-            }
-          }
-        }
-      }
-    } else {
-      outer_block<HS>(h, w);
-      if (on) {
-#pragma unroll
-        for (int k = 0; k < W; ++k) h[k] = opad[k];
-      }
-    }
-    uint32_t hn[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) hn[k] = h[k];
-    if (!(eopts() & 4)) Hash<HS>::compress(hn, w);
-    if (on) {
-#pragma unroll
-      for (int k = 0; k < W; ++k) h[k] = hn[k];
-    }
-    // chunk b's plaintext out of the tile, 4 lanes x 16 contiguous bytes per
-    // record: CBC blocks 4b-2 .. 4b+1 (0, 1 for b = 0) are record bytes
-    // [64b-8, 64b+56), CTR blocks 4b-1 .. 4b+2 (0..2) bytes [64b, 64b+64).
-    // Lane = record stores (16 B at 64 records per instruction) write the
-    // same lines in 4x the pieces and leave them half-written in L2.
-    if (!(eopts() & 8)) {
-      const uint32_t obase = CK == CK_CBC ? (b == 0 ? 24u : 64 * b - 8) : (b == 0 ? 16u : 64 * b);
-      const int np = CK == CK_CBC ? (b == 0 ? 2 : 4) : (b == 0 ? 3 : 4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int src = qb | t;
-        const uint32_t soff = (uint32_t)__shfl((int)off, src);
-        if (__shfl((int)full, src) && pi < np)
-          st16(out + soff + obase + 16 * pi, *reinterpret_cast<const uint4 *>(tile + tile_off(src, pi)));
-      }
-    }
-  }
-  uint32_t diff = 0;
-  if (act)
-    for (uint32_t k = 0; k < mlen / 4; ++k)
-      diff |= bswap32(h[k]) ^ *reinterpret_cast<const uint32_t *>(rec + L0 + 4 * k);
-  return act && diff == 0;
-}
-
-template <int CK>
-__device__ __forceinline__ bool fused_hs(int aalg, const uint8_t *rec, uint8_t *orec, uint32_t plen,
-                                         uint32_t mlen, bool esn, uint32_t esn_hi, uint32_t salt, kptr ipad,
-                                         kptr opad, kptr key, int nr, const uint8_t *lds, uint8_t *tile, uint8_t *out,
-                                         uint32_t off, uint32_t slot, bool act, uint32_t *trl) {
-  if (aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
-    return eta_decrypt_fused<CK, HS_SHA256>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds,
-                                            tile, out, off, slot, act, trl);
-  return eta_decrypt_fused<CK, HS_SHA1>(rec, orec, plen, mlen, esn, esn_hi, salt, ipad, opad, key, nr, lds, tile,
-                                        out, off, slot, act, trl);
-}
 
 // out: the digest as big-endian words (5 / 8 / 12 / 16 of them)
 __device__ __forceinline__ void hmac_any(int aalg, const uint8_t *rec, uint32_t L0, bool esn, uint32_t esn_hi,
@@ -1153,156 +812,34 @@ __device__ __forceinline__ void fill_pair(uint8_t *lds, uint32_t base, const uin
   }
 }
 
-// MODE 7 (out of place, one session per wave unit, HMAC-SHA1 / SHA2-256 or no
-// authentication): the verify pass and the block-parallel decrypt run
-// interleaved in one loop instead of one after the other.  Out of place the
-// plaintext of a record that fails verification is not used (its status says
-// EBADMSG, its trailer word is 0), so every valid record is decrypted without
-// waiting for its HMAC, as the GCM kernel's MODE 0 does.  Iteration it issues
-// decrypt pass it's loads, runs HMAC block it of every lane's record (lane =
-// record, VALU; its own loads wait behind the pass's), then pass it's AES
-// rounds (LDS) and stores: each phase's memory latency hides under the other
-// phase's work, and the wave keeps both the VALU and the LDS pipe busy.
-// Returns the lane's verification result.
-template <int HS>
-__device__ __forceinline__ bool eta_interleaved(const EtaParams &p, const uint8_t *lds, uint32_t slot, int lane,
-                                                bool run, uint32_t off, uint32_t plen, uint32_t hl, uint32_t di,
-                                                uint32_t salt, uint32_t esnh, const DevSA *s) {
-  constexpr int U = 4;                                         // aes_dec4 / aes_enc4 width
-  const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM, null = s->calg == ESPGPU_CRYPTO_NULL_CBC;   // wave-uniform
-  const int nr = (int)s->nr;
-  const uint32_t aalg = s->aalg, mlen = s->mlen;
-  const uint8_t *rec = p.arena + off;
-  // flat block list of the wave's records
-  const uint32_t nb = run ? (plen + 15) / 16 : 0;
-  uint32_t incl = nb;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  const uint32_t start = incl - nb;
-  const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
-  const int passes = (total + 64 * U - 1) / (64 * U);
-  // HMAC of rec[0, hl + plen) (|| ESN high word), hmac_t's block schedule
-  const bool esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
-  const uint32_t L0 = hl + plen, L = L0 + (esn ? 4u : 0u);
-  const uint32_t nfull = L0 / 64, htotal = (L + 9 + 63) / 64;
-  const uint64_t bits = (uint64_t)(64 + L) * 8;
-  const int hsteps = run && aalg != 0 ? (int)htotal + 1 : 0;
-  int hmax = hsteps;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) hmax = max(hmax, __shfl_xor(hmax, o));
-  uint32_t h[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) h[k] = k < Hash<HS>::W ? kp(s->ipad)[k] : 0u;
-  const int iters = max(passes, hmax);
-  for (int it = 0; it < iters; ++it) {
-    // (1) this pass's loads: blocks it*256 + lane + 64k of the flat list
-    int fk[U];
-    uint32_t ik[U], rok[U], rplk[U], rdik[U];
-    uint4 v[U], pv[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int f = it * 64 * U + lane + 64 * k;
-      int j = 0;
-      uint32_t sj = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1) {
-        const uint32_t sc = __shfl(start, j + step);
-        if ((int)sc <= f) {
-          j += step;
-          sj = sc;
-        }
-      }
-      fk[k] = f < total ? f : -1;
-      ik[k] = (uint32_t)f - sj;
-      rok[k] = __shfl(off, j);
-      rplk[k] = __shfl(plen, j);
-      rdik[k] = __shfl(di, j);
-      const uint32_t rs = __shfl(salt, j);
-      v[k] = pv[k] = make_uint4(0, 0, 0, 0);
-      if (fk[k] >= 0) {
-        const uint8_t *r = p.arena + rok[k];
-        if (null) {
-          v[k] = ld16(r + 8 + 16 * ik[k]);
-        } else if (ctr) {
-          pv[k] = ld16(r + 16 + 16 * ik[k]);
-          v[k] = make_uint4(rs, *reinterpret_cast<const uint32_t *>(r + 8),
-                            *reinterpret_cast<const uint32_t *>(r + 12), bswap32(ik[k] + 1));
-        } else {
-          v[k] = ld16(r + 24 + 16 * ik[k]);
-          pv[k] = ld16(r + 8 + 16 * ik[k]);
-        }
-      }
-    }
-    // (2) one HMAC block per lane
-    if (it < hsteps) hmac_step<HS>(h, rec, (uint32_t)it, nfull, htotal, L0, L, esn, esnh, bits, kp(s->opad));
-    // (3) the pass's rounds and stores
-    if (it < passes) {
-      if (null) {
-      } else if (ctr) {
-        aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
-      } else {
-        aes_dec4(v, kp(s->dk), nr, lds, slot);
-      }
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        if (fk[k] >= 0) {
-          uint8_t *dst = p.out + rok[k];
-          const uint32_t i = ik[k], rpl = rplk[k];
-          const int rem = (int)rpl - 16 * (int)i;
-          const uint4 pt = xor4(v[k], pv[k]);
-          if (null) st_partial(dst + 8 + 16 * i, pt, rem);
-          else if (ctr) st_partial(dst + 16 + 16 * i, pt, rem);
-          else st16(dst + 24 + 16 * i, pt);
-          if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdik[k]] = esp_trailer_word(last_word(pt, rem), rpl);
-        }
-      }
-    }
-  }
-  if (!run) return false;
-  if (aalg == 0) return true;                                  // CSP_MODE_CIPHER: nothing to verify
-  uint32_t diff = 0;
-  for (uint32_t k = 0; k < mlen / 4; ++k)
-    diff |= bswap32(h[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
-  return diff == 0;
-}
-
-// MODE 0: decrypt out-of-place, one fused pass (SHA-1 / SHA2-256 sessions of
-// one cipher; used only with set_tuning eta_fused = 1); 1: encrypt in place,
-// MAC pass; 2: decrypt in place (verify first); 3: decrypt out of place,
-// verify pass then the block-parallel pass of MODE 2 writing to p.out -- with
-// p.two_pass_all (eta_fused = 2, the default) for every ETA session, else only
-// for the SHA2-384/512 sessions (128-byte hash blocks do not line up with
-// MODE 0's four-block chunks); 4: encrypt, cipher pass; 5 / 6: the separate
-// decrypt / verify kernels (eta_fused = 0)
-// CKS: MODE 0 is built once per cipher (CK_CBC / CK_CTR) and each launch
-// serves only its cipher's sessions -- both fused paths inlined in one kernel
-// made the register allocator spill; -1 = every ETA session.
-#ifndef ETA_C8_WG
-#define ETA_C8_WG 512
-#endif
+// MODE 1: encrypt, MAC pass over the ciphertext MODE 4 wrote (lane = record
+//         HMAC, ICV written);
+// MODE 2: decrypt in place, verify first: the verify pass (lane = record
+//         HMAC), then the block-parallel decrypt of the verified records;
+// MODE 3: decrypt out of place: the same two passes, plaintext to p.out;
+// MODE 4: encrypt, cipher pass (lane = record CBC chain / CTR keystream).
+// CKS: MODE 4 is built once per cipher (CK_CBC / CK_CTR); MODE 1 / 2 / 3 once
+// per hash width (CK_NARROW: HMAC-SHA1 / SHA2-256 / no auth, no SHA-512 code,
+// so the registers fit without spilling; CK_WIDEH: HMAC-SHA2-384/512).
+// (Measured slower and not built: the one-pass out-of-place decrypt, the
+// verify and decrypt passes as separate kernels, side by side on two streams,
+// or interleaved per wave; the in-place one pass with CBC rollback:
+// DESIGN.md §3.2, §5.1, §6.)
 template <int MODE, int WG, int CKS>
-__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? ETA_ENC_WPE : 1) void eta_kernel(EtaParams p) {
+__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_kernel(EtaParams p) {
+  static_assert(MODE >= 1 && MODE <= 4, "MAC pass, in-place / out-of-place decrypt, cipher pass");
+  // (MODE 4 CBC: at least 8 waves per SIMD, <= 64 VGPRs, two workgroups per CU)
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
   if (MODE == 4) {
     fill_pair(lds, LDS_T, p.tpair, tid, WG);
-  } else if (MODE != 1 && MODE != 6) {            // MODE 1 / 6 (MAC passes) read no table
-    // a MODE 0 kernel serves one cipher: CBC needs Td + the inverse S-box and
-    // stages plaintext where Te would be, CTR needs Te and stages in Td's place
-    if (MODE != 0 || CKS != CK_CTR) {
-      fill_pair(lds, LDS_T, p.dpair, tid, WG);
-      for (int idx = tid; idx < 256 * 32; idx += WG)
-        *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[idx >> 5];
-    }
-    if (MODE != 0 || CKS != CK_CBC) fill_pair(lds, LDS_TE, p.tpair, tid, WG);
+  } else if (MODE != 1) {                         // MODE 1 (the MAC pass) reads no table
+    fill_pair(lds, LDS_T, p.dpair, tid, WG);
+    for (int idx = tid; idx < 256 * 32; idx += WG)
+      *reinterpret_cast<uint32_t *>(lds + LDS_SI + idx * 4) = p.isbox[idx >> 5];
+    fill_pair(lds, LDS_TE, p.tpair, tid, WG);
   }
-  static_assert((WG / 64) * 4096 <= 65536, "plaintext tiles fit the unused table region");
-  uint8_t *tile = lds + (CKS == CK_CTR ? LDS_T : LDS_TE) +
-                  (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6) * 4096u;   // wave-uniform (MODE 0)
   __syncthreads();
 
   // Work units are one wave's worth of records: a 64-record ETA chunk of one
@@ -1311,17 +848,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
   const bool implicit = p.chunks == nullptr;
   const uint32_t u0 = implicit ? 0u : p.nchunks[0];
   const uint32_t u1 = implicit ? (p.n + 63) / 64 : p.nchunks[1];
-  if (ETA_STAGGER && MODE == 2) {
-    // probe: start some waves late so the waves of a CU are not all in the
-    // same phase (verify: memory + VALU; decrypt: LDS) at the same time
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint64_t d = ETA_STAGGER_MODE ? (uint64_t)(w & 3) * ETA_STAGGER : (uint64_t)(w & 1) * ETA_STAGGER;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
-  }
   for (;;) {
     uint32_t t = 0;
-    if (lane == 0) t = ETA_XCDQ ? xcd_ticket(p.queue, blockIdx.x & 7u, u1 - u0) : atomicAdd(&p.queue[0], 1u);
+    if (lane == 0) t = atomicAdd(&p.queue[0], 1u);
     const uint32_t u = u0 + __builtin_amdgcn_readfirstlane(t);
     if (u >= u1) break;
     uint32_t di = 0;
@@ -1337,7 +866,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
     // ---- lane = record: descriptor, HMAC (verify or compute) ----
     bool valid = false, ok = false;
     uint32_t off = 0, len = 0, sa = 0, plen = 0, hl = 24, salt = 0, esnh = 0;
-    int hq = 0;                                  // ETA_HMAC_QUAD: 1 SHA-1 / 2 SHA2-256 record to hash
+    int hq = 0;                                  // MODE 2 narrow: 1 SHA-1 / 2 SHA2-256 record to hash
     bool hq_esn = false;
     uint32_t hq_mlen = 0;
     if (have) {
@@ -1354,18 +883,10 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
           p.status[di] = ESPGPU_EINVAL;
           if (MODE != 1 && p.trailer) p.trailer[di] = 0;
         }
-      } else if (MODE == 0 && ((s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR) ||
-                               two_pass_only(s->calg, s->aalg))) {
-        have = false;                                       // another decrypt launch's session
       } else if (MODE == 4 && (s->calg == ESPGPU_CRYPTO_NULL_CBC ||
                                (s->calg == ESPGPU_CRYPTO_AES_ICM) != (CKS == CK_CTR))) {
         have = false;                                       // the other cipher's pass / no cipher
-      } else if (MODE == 3 && !two_pass_only(s->calg, s->aalg) && !p.two_pass_all) {
-        have = false;                                       // the fused launches' session
-      } else if ((MODE == 5 || MODE == 6 || MODE == 8) && two_pass_only(s->calg, s->aalg)) {
-        have = false;                                       // MODE 3's session
-      } else if ((MODE == 1 || MODE == 2 || MODE == 3 || MODE == 7) && ((CKS == CK_NARROW && wide_hash(s->aalg)) ||
-                                              (CKS == CK_WIDEH && !wide_hash(s->aalg)))) {
+      } else if (MODE != 4 && ((CKS == CK_NARROW && wide_hash(s->aalg)) || (CKS == CK_WIDEH && !wide_hash(s->aalg)))) {
         have = false;                                       // the other hash set's launch
       } else {
         const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM, null = s->calg == ESPGPU_CRYPTO_NULL_CBC;
@@ -1377,21 +898,19 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
         // multiples)
         valid = pl > 0 && (ctr || null || (pl & 15) == 0) && (len & 3) == 0;
         plen = valid ? (uint32_t)pl : 0;
-        if (valid && MODE == 5) ok = p.status[di] == ESPGPU_OK;   // verified by the MODE 6 pass
-        if (valid && MODE == 8) ok = true;          // decrypt every valid record (MODE 6 verifies beside it)
-        if (valid && (MODE == 2 || MODE == 3 || MODE == 6 || MODE == 7) && s->aalg == 0) {
+        if (valid && (MODE == 2 || MODE == 3) && s->aalg == 0) {
           ok = true;                                        // CSP_MODE_CIPHER: nothing to verify
         } else if (valid && (MODE == 2 || MODE == 3) && (eopts() & 0x10000)) {
           ok = true;                                        // knob: no verify pass at all
-        } else if (ETA_HMAC_QUAD && valid && MODE == 2 && CKS == CK_NARROW) {
+        } else if (valid && MODE == 2 && CKS == CK_NARROW) {
           hq = s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 1;   // hashed below, by the whole wave
           hq_esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
           hq_mlen = mlen;
-        } else if (valid && (MODE == 2 || MODE == 3 || MODE == 6)) {
+        } else if (valid && (MODE == 2 || MODE == 3)) {
           uint32_t dg[16];
           const uint8_t *rec = p.arena + off;
-          if (MODE == 6 || CKS == CK_NARROW) {   // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
-            if (!ETA_PROBE_SHA1ONLY && s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+          if (CKS == CK_NARROW) {              // SHA-1 / SHA2-256 only: no SHA-512 code, fewer VGPRs
+            if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
               hmac_t<HS_SHA256>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad),
                                 kp(s->opad), dg);
             else
@@ -1408,8 +927,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
         }
       }
     }
-    if (ETA_HMAC_QUAD && MODE == 2 && CKS == CK_NARROW) {
+    if (MODE == 2 && CKS == CK_NARROW) {
       // the verify of this unit's records, the whole wave at once
+      // (hmac_quad: quad-coalesced loads, two hash blocks per load)
       for (int hs = 1; hs <= 2; ++hs) {           // (not unrolled: two hmac_quad bodies)
         if (!__any(hq == hs)) continue;           // wave-uniform
         const bool act = hq == hs;
@@ -1417,9 +937,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
         const uint8_t *rec = p.arena + off;
         uint32_t dg[16];
         if (hs == 2)
-          hmac_quad<HS_SHA256, ETA_HQ_NB2>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
+          hmac_quad<HS_SHA256, 2>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
         else
-          hmac_quad<HS_SHA1, ETA_HQ_NB2>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
+          hmac_quad<HS_SHA1, 2>(act, rec, hl + plen, hq_esn, esnh, kp(s->ipad), kp(s->opad), dg);
         if (act) {
           uint32_t diff = 0;
           for (uint32_t k = 0; k < hq_mlen / 4; ++k)
@@ -1447,47 +967,25 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
         run = run && !mine;
         const DevSA *s = p.sas + sau;
         const int nr = (int)s->nr;
-        if (CKS == CK_CBC && ETA_ENC_QUAD4) {       // (the whole wave)
-          cbc_enc_quad<ETA_ENC_NB>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
+        if (CKS == CK_CBC) {                      // (the whole wave: quad-coalesced 64-byte groups)
+          cbc_enc_quad<1>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
           continue;
         }
         if (!mine) continue;
         uint8_t *rec = p.arena + off;
-        if (CKS == CK_CTR) {
-          const uint32_t iv0 = *reinterpret_cast<const uint32_t *>(rec + 8);
-          const uint32_t iv1 = *reinterpret_cast<const uint32_t *>(rec + 12);
-          const uint32_t nb = (plen + 15) / 16;
-          for (uint32_t b = 0; b < nb; b += 4) {
-            uint4 ks[4];
+        const uint32_t iv0 = *reinterpret_cast<const uint32_t *>(rec + 8);
+        const uint32_t iv1 = *reinterpret_cast<const uint32_t *>(rec + 12);
+        const uint32_t nb = (plen + 15) / 16;
+        for (uint32_t b = 0; b < nb; b += 4) {
+          uint4 ks[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) ks[k] = make_uint4(salt, iv0, iv1, bswap32(b + (uint32_t)k + 1));
-            aes_enc4(ks, kp(s->rk), nr, lds, slot);
+          for (int k = 0; k < 4; ++k) ks[k] = make_uint4(salt, iv0, iv1, bswap32(b + (uint32_t)k + 1));
+          aes_enc4(ks, kp(s->rk), nr, lds, slot);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (b + k < nb)
-                st_partial(rec + 16 + 16 * (b + k), xor4(ld16(rec + 16 + 16 * (b + k)), ks[k]),
-                           (int)(plen - 16 * (b + k)));
-          }
-        } else {
-          // four blocks (64 contiguous bytes) per load and per store: the
-          // record is streamed in 64-byte pieces, not 16
-          uint4 prev = ld16(rec + 8);                       // IV
-          const uint32_t nb = plen / 16;
-          for (uint32_t b = 0; b < nb; b += 4) {
-            uint4 m[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) m[k] = b + k < nb ? ld16(rec + 24 + 16 * (b + k)) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              if (b + k < nb) {
-                prev = aes_enc(xor4(m[k], prev), kp(s->rk), nr, lds, slot);
-                m[k] = prev;
-              }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (b + k < nb) st16(rec + 24 + 16 * (b + k), m[k]);
-          }
+          for (int k = 0; k < 4; ++k)
+            if (b + k < nb)
+              st_partial(rec + 16 + 16 * (b + k), xor4(ld16(rec + 16 + 16 * (b + k)), ks[k]),
+                         (int)(plen - 16 * (b + k)));
         }
       }
       continue;
@@ -1498,22 +996,22 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
       // SHA-1 / SHA2-256 ICVs with hmac_quad's coalesced block loads (the whole
       // wave calls it), SHA2-384/512 with hmac_any
       int hq1 = 0;
-      if (ETA_ENC_QUAD && have && valid) {
+      if (have && valid) {
         const uint32_t aa = p.sas[sa].aalg;
         hq1 = aa == ESPGPU_CRYPTO_SHA1_HMAC ? 1 : aa == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 0;
       }
       for (int hs = 1; hs <= 2; ++hs) {           // (not unrolled: two hmac_quad bodies)
-        if (!ETA_ENC_QUAD || !__any(hq1 == hs)) continue;     // wave-uniform
+        if (!__any(hq1 == hs)) continue;          // wave-uniform
         const bool act = hq1 == hs;
         const DevSA *s = p.sas + (act ? sa : 0u);
         uint8_t *rec = p.arena + off;
         uint32_t dg[16];
         if (hs == 2)
-          hmac_quad<HS_SHA256, ETA_HQ_NB1>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh,
-                                           kp(s->ipad), kp(s->opad), dg);
+          hmac_quad<HS_SHA256, 2>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh,
+                                  kp(s->ipad), kp(s->opad), dg);
         else
-          hmac_quad<HS_SHA1, ETA_HQ_NB1>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh,
-                                         kp(s->ipad), kp(s->opad), dg);
+          hmac_quad<HS_SHA1, 2>(act, rec, hl + plen, act && (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh,
+                                kp(s->ipad), kp(s->opad), dg);
         if (act)
           for (uint32_t k = 0; k < s->mlen / 4; ++k)
             *reinterpret_cast<uint32_t *>(rec + hl + plen + 4 * k) = bswap32(dg[k]);
@@ -1530,77 +1028,13 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
       if (have) p.status[di] = valid ? ESPGPU_OK : ESPGPU_EINVAL;
       continue;
     }
-    if (MODE == 0) {
-      // ---- out-of-place decrypt: one fused pass per record (lane = record),
-      // one session at a time so round keys and pads stay in SGPRs ----
-      bool run = have && valid;
-      uint64_t todo = __ballot(run);
-      while (todo) {
-        const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
-        const bool mine = run && sa == sau;
-        todo &= ~__ballot(mine);
-        run = run && !mine;
-        const DevSA *s = p.sas + sau;
-        uint32_t trl = 0;
-        const bool esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
-        const uint32_t roff = (eopts() & 1) ? (off & 0xffffcu) : off;
-        const bool good = fused_hs<CKS == CK_CTR ? CK_CTR : CK_CBC>(
-            (int)s->aalg, p.arena + roff, p.out + roff, plen, s->mlen, esn, esnh, salt, kp(s->ipad), kp(s->opad),
-            kp(CKS == CK_CTR ? s->rk : s->dk), (int)s->nr, lds, tile, p.out, roff, slot, mine, &trl);
-        if (mine) {
-          ok = good;
-          if (p.trailer) p.trailer[di] = good ? trl : 0u;
-        }
-      }
-      if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
-      if (have && p.trailer && !valid) p.trailer[di] = 0;
-      continue;
-    }
-    if (MODE == 7) {
-      // one session in the unit (planner chunks): verify and decrypt
-      // interleaved; otherwise verify here and take MODE 3's path below
-      const bool run = have && valid;
-      const uint64_t rm = __ballot(run);
-      const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, rm ? __builtin_ctzll(rm) : 0));
-      if (rm && __all(!run || sa == sau)) {
-        const DevSA *s = p.sas + sau;
-        const bool good = s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC
-                              ? eta_interleaved<HS_SHA256>(p, lds, slot, lane, run, off, plen, hl, di, salt, esnh, s)
-                              : eta_interleaved<HS_SHA1>(p, lds, slot, lane, run, off, plen, hl, di, salt, esnh, s);
-        if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (good ? ESPGPU_OK : ESPGPU_EBADMSG);
-        if (p.trailer) {
-          // another lane of this wave may have written the record's trailer
-          // word in a decrypt pass: order that store before the zeroing
-          __threadfence_block();
-          if (have && !(valid && good)) p.trailer[di] = 0;
-        }
-        continue;
-      }
-      if (run && p.sas[sa].aalg != 0) {
-        const DevSA *s = p.sas + sa;
-        uint32_t dg[16];
-        const uint8_t *rec = p.arena + off;
-        if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
-          hmac_t<HS_SHA256>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad), kp(s->opad), dg);
-        else
-          hmac_t<HS_SHA1>(rec, hl + plen, (s->flags & ESPGPU_CSP_F_ESN) != 0, esnh, kp(s->ipad), kp(s->opad), dg);
-        uint32_t diff = 0;
-        for (uint32_t k = 0; k < s->mlen / 4; ++k)
-          diff |= bswap32(dg[k]) ^ *reinterpret_cast<const uint32_t *>(rec + hl + plen + 4 * k);
-        ok = diff == 0;
-      }
-    }
-    if (MODE == 6) {                // verify pass: status only; MODE 5 decrypts what passed
-      if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
-      continue;
-    }
-    if (have && MODE != 5 && MODE != 8) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
+    if (have) p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
     // trailer word: 0 now for records that will not be decrypted; the lane
     // decrypting a record's last block writes the others'
     if (have && p.trailer && !(valid && ok)) p.trailer[di] = 0;
 
-    // ---- verified in-place decrypt: all of the wave's blocks of one session
-    // as one flat list ----
+    // ---- verified decrypt: all of the wave's blocks of one session as one
+    // flat list ----
     // Records to decrypt (one session at a time, so the round keys stay
     // wave-uniform in SGPRs) are concatenated; every lane takes one block per
     // pass, last pass first.  Within a pass all lanes load their blocks (and
@@ -1627,9 +1061,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
       const uint32_t start = incl - nb;
       const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
       const int nr = (int)s->nr;
-      // U blocks per lane per pass, 64 apart (each load instruction covers
-      // 64 consecutive blocks), decrypted together for ILP
-      constexpr int U = ETA_U;
+      // kEtaU blocks per lane per pass, 64 apart (each load instruction
+      // covers 64 consecutive blocks), decrypted together for ILP
+      constexpr int U = kEtaU;
       for (int base = total - 64 * U; base > -64 * U; base -= 64 * U) {
         int fk[U];
         uint32_t ik[U], rok[U], rplk[U], rdik[U], rsk[U];
@@ -1637,46 +1071,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
         for (int k = 0; k < U; ++k) {
           const int f = base + lane + 64 * k;
           // the record holding flat block f: the last lane whose start <= f
+          // (6-step shuffle search; by ballot and v_readlane it measured equal)
           int j = 0;
           uint32_t sj = 0;
-#if ETA_LANE_MAP
-          // The pass's 64 blocks of this k are one window [F, F + 63]: the
-          // record of its first block from a ballot (no LDS), and when at
-          // most three more records start inside the window (records of >= 22
-          // blocks; ties of lanes without blocks included) each lane's record
-          // is one of four, read with v_readlane: no ds_bpermute for the
-          // search or the record's offset (they share the LDS pipe with the
-          // AES lookups).  Otherwise the shuffle search below.
-          const int F = base + 64 * k, Fc = F < 0 ? 0 : F;
-          const int j0 = (int)__builtin_popcountll(__ballot((int)start <= Fc)) - 1;
-          auto rl = [&](uint32_t v, int jj) { return (uint32_t)__builtin_amdgcn_readlane((int)v, jj > 63 ? 63 : jj); };
-          const int s1 = j0 + 1 > 63 ? INT32_MAX : (int)rl(start, j0 + 1);
-          const int s2 = j0 + 2 > 63 ? INT32_MAX : (int)rl(start, j0 + 2);
-          const int s3 = j0 + 3 > 63 ? INT32_MAX : (int)rl(start, j0 + 3);
-          const int s4 = j0 + 4 > 63 ? INT32_MAX : (int)rl(start, j0 + 4);
-          const bool fast = s4 > F + 63;                              // wave-uniform
-          int m = 0;
-          if (fast) {
-            m = (f >= s1) + (f >= s2) + (f >= s3);
-            j = j0 + m;
-            const uint32_t st0 = rl(start, j0);
-            sj = m == 0 ? st0 : (m == 1 ? (uint32_t)s1 : (m == 2 ? (uint32_t)s2 : (uint32_t)s3));
-            const uint32_t o0 = rl(off, j0), o1 = rl(off, j0 + 1), o2 = rl(off, j0 + 2), o3 = rl(off, j0 + 3);
-            rok[k] = m == 0 ? o0 : (m == 1 ? o1 : (m == 2 ? o2 : o3));
-          } else {
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1) {
-              const uint32_t sc = __shfl(start, j + step);
-              if ((int)sc <= f) {
-                j += step;
-                sj = sc;
-              }
-            }
-            rok[k] = __shfl(off, j);
-          }
-          fk[k] = f;
-          ik[k] = (uint32_t)f - sj;
-#else
 #pragma unroll
           for (int step = 32; step >= 1; step >>= 1) {
             const uint32_t sc = __shfl(start, j + step);
@@ -1688,18 +1085,11 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
           fk[k] = f;
           ik[k] = (uint32_t)f - sj;
           rok[k] = __shfl(off, j);
-#endif
-#if ETA_LEAN_SHFL
           // (each __shfl is a ds_bpermute on the LDS pipe the AES lookups
           // bound: only what the session kind uses, wave-uniform conditions)
           rplk[k] = (ctr || null || p.trailer) ? __shfl(plen, j) : 0u;
           rdik[k] = p.trailer ? __shfl(di, j) : 0u;
           rsk[k] = ctr ? __shfl(salt, j) : 0u;
-#else
-          rplk[k] = __shfl(plen, j);
-          rdik[k] = __shfl(di, j);
-          rsk[k] = __shfl(salt, j);
-#endif
         }
         // all loads of the pass before any store (in place: see above)
         uint4 v[U], pv[U];
@@ -1729,7 +1119,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
 #pragma unroll
         for (int k = 0; k < U; ++k) {
           if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass stores
-            uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3 / 5 / 7: p.out (may be p.arena)
+            uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3: p.out (may be p.arena)
             const uint32_t i = ik[k], rpl = rplk[k];
             const int rem = (int)rpl - 16 * (int)i;
             const uint4 pt = xor4(v[k], pv[k]);
@@ -1750,11 +1140,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC && ETA_ENC_QUAD4 ? E
   // all have retired no ticket is drawn again: reset for the next launch.
   if (lane == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x * (WG / 64) - 1) {
     atomicExch(&p.queue[0], 0u);
-    if (ETA_XCDQ) xcd_reset(p.queue);
     atomicExch(&p.queue[1], 0u);
   }
 }
-
 
 }  // namespace
 
@@ -1766,16 +1154,12 @@ int set_eta_opts(uint32_t opts) {
 #endif
 }
 
-// 768-thread workgroups: 3 waves/SIMD at up to 170 VGPRs (the unrolled hash
-// schedules need ~150); decrypt takes 160 KiB of LDS, one workgroup per CU.
-// The concurrent design's trailer merge: MODE 8 wrote a trailer word for
-// every valid record, MODE 6 the statuses; a record that failed keeps 0.
-__global__ __launch_bounds__(256) void eta_trailer_merge(const uint8_t *status, uint32_t *trailer, uint32_t n) {
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-    if (status[i] != ESPGPU_OK) trailer[i] = 0;
-}
-
-int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream, const EtaAux *aux) {
+// Decrypt: 160 KiB of LDS, one workgroup per CU; the in-place SHA-1 /
+// SHA2-256 launch at 1024 threads (hmac_quad: 128 VGPRs, 4 waves/SIMD), the
+// others at 768 (3 waves/SIMD at up to 170 VGPRs: the unrolled hash schedules
+// need ~150).  Encrypt: the cipher passes at 1024 threads, up to two
+// workgroups per CU, then the MAC pass.
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   // implicit units (64 records, one wave each): no more workgroups than units
@@ -1785,85 +1169,20 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, 
     return std::max(1, std::min(g, (units + wpg - 1) / wpg));
   };
   const int in_place = !encrypt && p.out == p.arena;
-  // kinds: bit 0 = SHA-1 / SHA2-256 CBC sessions exist, bit 1 = such CTR
-  // sessions, bits 2/3 = SHA2-384/512 CBC / CTR sessions
   if (encrypt) {
-    // cipher passes (lean, 1024 threads, up to 2 workgroups per CU), then the MAC pass
     if (kinds & 5)
       hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
     if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
-    // MAC pass by hash width, as the in-place decrypt: SHA-1 / SHA2-256 / no
-    // auth without the SHA-512 code (1024 threads), SHA2-384/512 apart
-    hipLaunchKernelGGL((eta_kernel<1, ETA_WG1, CK_NARROW>), dim3(clamp(grid, ETA_WG1)), dim3(ETA_WG1), 0, st, p);
+    // MAC pass by hash width, as the decrypt: SHA-1 / SHA2-256 / no auth
+    // without the SHA-512 code (1024 threads), SHA2-384/512 apart
+    hipLaunchKernelGGL((eta_kernel<1, 1024, CK_NARROW>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
     if (kinds & 16) hipLaunchKernelGGL((eta_kernel<1, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-  } else if (fused) {
-    // in place: the verify-first kernel (MODE 2); out of place: MODE 3 for
-    // every session (eta_fused = 2, the default), or the one-pass MODE 0
-    // kernel per cipher plus MODE 3 for SHA2-384/512 (eta_fused = 1)
-    // (kinds bit 4: HMAC-SHA2-384/512 sessions exist, served by their own launch)
-    if (in_place) {
-#if defined(ESPGPU_VARIANTS) && defined(ETA_INPLACE_PROBE)
-      // timing probe only (no rollback of failed records): the one-pass MODE 0
-      // over the records in place
-      if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      return hipGetLastError() == hipSuccess ? 0 : -1;
-#endif
-      hipLaunchKernelGGL((eta_kernel<2, ETA_WG2, CK_NARROW>), dim3(clamp(grid, ETA_WG2)), dim3(ETA_WG2), 0, st, p);
-      if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-#ifdef ESPGPU_VARIANTS
-    } else if (fused == 4 && aux) {
-      // concurrent (eta_fused 4, out of place): the verify pass (MODE 6, lane
-      // = record SHA-1 / SHA2-256 on the VALU, no LDS) on the aux stream beside
-      // the decrypt of every valid record (MODE 8, block-parallel AES on the
-      // LDS tables), sized to share each CU (2 decrypt waves + 1 verify wave
-      // per SIMD); SHA2-384/512 sessions after them (MODE 3)
-      hipStream_t sa = reinterpret_cast<hipStream_t>(aux->aux);
-      hipEvent_t ef = reinterpret_cast<hipEvent_t>(aux->ev_fork), ej = reinterpret_cast<hipEvent_t>(aux->ev_join);
-      EtaParams pv = p;
-      pv.queue = aux->queue;
-      if (hipEventRecord(ef, st) != hipSuccess || hipStreamWaitEvent(sa, ef, 0) != hipSuccess) return -1;
-      if (kinds & 3) {
-        hipLaunchKernelGGL((eta_kernel<8, ETA_C8_WG, -1>), dim3(clamp(grid, ETA_C8_WG)), dim3(ETA_C8_WG), 0, st, p);
-        hipLaunchKernelGGL((eta_kernel<6, 256, -1>), dim3(clamp(grid, 256)), dim3(256), 0, sa, pv);
-      }
-      if (hipEventRecord(ej, sa) != hipSuccess || hipStreamWaitEvent(st, ej, 0) != hipSuccess) return -1;
-      if ((kinds & 3) && p.trailer)
-        hipLaunchKernelGGL(eta_trailer_merge, dim3(std::min(1024u, (p.n + 255) / 256)), dim3(256), 0, st, p.status,
-                           p.trailer, p.n);
-      if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-#endif
-    } else if (p.two_pass_all && !p.interleave) {
-      hipLaunchKernelGGL((eta_kernel<3, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
-      if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-    } else {
-#ifdef ESPGPU_VARIANTS
-      // measured-slower designs, variants library only
-      if (p.two_pass_all) {
-        hipLaunchKernelGGL((eta_kernel<7, ETA_WG3, CK_NARROW>), dim3(clamp(grid, ETA_WG3)), dim3(ETA_WG3), 0, st, p);
-        if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      } else {
-        if (kinds & 1) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CBC>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-        if (kinds & 2) hipLaunchKernelGGL((eta_kernel<0, 768, CK_CTR>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-        if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-      }
-#else
-      return -1;
-#endif
-    }
+  } else if (in_place) {
+    hipLaunchKernelGGL((eta_kernel<2, 1024, CK_NARROW>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
+    if (kinds & 16) hipLaunchKernelGGL((eta_kernel<2, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   } else {
-#ifdef ESPGPU_VARIANTS
-    // verify pass (lane = record HMAC, status), then the block-parallel
-    // decrypt of the records that passed, in place or out of place: two lean
-    // kernels, each at the occupancy its own registers allow
-    if (kinds & 3) {
-      hipLaunchKernelGGL((eta_kernel<6, 768, -1>), dim3(clamp(2 * grid, 768)), dim3(768), 0, st, p);
-      hipLaunchKernelGGL((eta_kernel<5, 1024, -1>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
-    }
-    if (kinds & 12) hipLaunchKernelGGL((eta_kernel<3, 768, CK_ALL>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
-#else
-    return -1;
-#endif
+    hipLaunchKernelGGL((eta_kernel<3, 768, CK_NARROW>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
+    if (kinds & 16) hipLaunchKernelGGL((eta_kernel<3, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

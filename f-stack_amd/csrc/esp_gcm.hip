@@ -49,104 +49,20 @@
 #include <algorithm>
 
 #include "espgpu_internal.h"
-#include "aes_bs.h"
 #include "xfer_copy.h"
-
-// Experiment switches (tools/variant.sh builds; defaults are the product)
-#ifndef GCM_SMALL_CHUNK_WAVES
-#define GCM_SMALL_CHUNK_WAVES 1
-#endif
-#ifndef GCM_PREFETCH
-#define GCM_PREFETCH 0
-#endif
-#ifndef GCM_STORE_LATE
-#define GCM_STORE_LATE 0
-#endif
-#ifndef GCM_WG
-#define GCM_WG 1024
-#endif
-#ifndef GCM_CTR_SINGLE
-#define GCM_CTR_SINGLE 0
-#endif
-#ifndef GCM_BS_VGPRS
-#define GCM_BS_VGPRS 192
-#endif
-#ifndef GCM_SPLIT_WPE
-#define GCM_SPLIT_WPE 4
-#endif
-#ifndef GCM_ALIGNED
-#define GCM_ALIGNED 1
-#endif
-#ifndef GCM_OUTALIGN
-#define GCM_OUTALIGN 0
-#endif
-// Output ring (MODE 0, S = 4, 1024-thread workgroups): plaintext goes through
-// a 128-byte LDS line buffer per record and leaves as whole 128-byte lines
-#ifndef GCM_RING
-#define GCM_RING 0
-#endif
-#ifndef GCM_H4_LDS
-#define GCM_H4_LDS 1  // session change: the 4-bit power table through LDS (stage_h8_lds)
-#endif
-#ifndef GCM_STAGE_INL
-// the cold work of the chunk loop (session-change table staging, the first
-// T-table fill, MODE 3's rollback of a failed record) as real calls: kept
-// out of the record loop's register allocation (gcm_kernel<3,1024,4>: 16 ->
-// 0 VGPRs spilled)
-#define GCM_STAGE_INL __noinline__
-#endif
-#ifndef GCM_FMU
-#define GCM_FMU 1     // throughput kernel's final multiply: words per L2 round trip (1, 2 or 4)
-#endif
-#ifndef GCM_XCDQ2
-#define GCM_XCDQ2 0  // per-XCD work-queue tickets (xcd_ticket) in gcm_kernel
-#endif
-// In-place decrypt, verify first (fused kernel, S = 4 and 8): 1 = one pass that decrypts
-// in place while hashing and rolls a failed record back (CTR is its own
-// inverse: the same keystream XORed over the plaintext restores the
-// ciphertext bit for bit); 0 = MODE 2's two passes (GHASH + tag, then CTR
-// over the authenticated records only)
-#ifndef GCM_INPLACE_ONEPASS
-#define GCM_INPLACE_ONEPASS 1
-#endif
-// Final multiply from LDS (planner batches, S = 4 kernel): lane 0's H^4 from
-// the resident 8-bit table, lanes 1-3's H^3..H^1 from 4-bit tables staged
-// value-major (24 KiB) with the session's GHASH table, instead of gathers of
-// the 32 KiB power tables from L2 (which miss once a batch has many sessions)
-#ifndef GCM_FMUL_LDS
-#define GCM_FMUL_LDS 0
-#endif
-// Hybrid AES (throughput kernel, AES-128): every GCM_HYBRID-th interior pair
-// step's 8 counter blocks of a record are computed by the record's 4 lanes
-// bitsliced on the VALU (aes_ctr8_bsq) instead of by T-table lookups on the
-// LDS pipe, which bounds the kernel; 0 = T-tables only.
-#ifndef GCM_HYBRID
-#define GCM_HYBRID 0
-#endif
-#ifndef GCM_HYBRID_PRIO
-#define GCM_HYBRID_PRIO 0
-#endif
 
 namespace espgpu {
 
 namespace {
-constexpr int kGcmInPlaceMode = GCM_INPLACE_ONEPASS ? 3 : 2;   // do_group MODE of an in-place decrypt
+constexpr int kGcmInPlaceMode = 3;     // do_group MODE of an in-place decrypt (one pass, verify-first)
 
 // LDS: the 8-bit H^S GHASH table at 0 (value-major, gf_mul8), the AES
 // T-table at 64 KiB.
 constexpr uint32_t LDS_GT = 0;          // H^S, 256 values x 16 positions x 16 B
 constexpr uint32_t LDS_TP = 65536;      // 256 entries x 32 lane slots x 8 B
 constexpr uint32_t LDS_BYTES = LDS_TP + 65536;
-constexpr uint32_t LDS_FM = LDS_BYTES;     // GCM_FMUL_LDS: H^1..H^3 4-bit tables, value-major
-constexpr uint32_t kFmBytes = 3 * kGhPowerBytes;
-// The output ring after them (gcm_kernel with RING): 128 bytes per record in
-// flight, 256 records per workgroup = the 32 KiB the tables leave of 160 KiB.
-constexpr uint32_t LDS_RING = LDS_BYTES;
-constexpr uint32_t kRingBytes = 128 * 256;
-// GCM_HYBRID: the session's round keys 1..10 as bit planes, [round][row][plane]
-constexpr uint32_t LDS_KP = LDS_BYTES;
-constexpr uint32_t kKpBytes = 10 * 4 * 8 * 4;
-constexpr int kHyb = GCM_HYBRID > 0 ? GCM_HYBRID : 1;   // one pair step in kHyb is bitsliced
+// then the staging scratch of a session change (stage_h8_lds): one 4-bit power table
+constexpr uint32_t LDS_ALL = LDS_BYTES + kGhPowerBytes;
 
 // Round keys are read through the constant address space: uniform loads from
 // it become s_load (SGPRs, scalar cache) instead of vector loads or LDS reads.
@@ -170,52 +86,18 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return perm(x, x, 0x00
 // operations (one IR access each, so the backend never splits or re-merges them)
 typedef uint32_t V4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t V2a __attribute__((ext_vector_type(2), aligned(4)));
-// GCM_NT (measurement switch): bit 0 = nontemporal record loads, bit 1 =
-// nontemporal stores (the streaming hint on the vector memory instructions)
-#ifndef GCM_NT
-#define GCM_NT 0
-#endif
+// (nontemporal hints on these measured 4-14 % slower: DESIGN.md §6)
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-#if GCM_NT & 1
-  const V4a v = __builtin_nontemporal_load(reinterpret_cast<const V4a *>(p));
-#else
   const V4a v = *reinterpret_cast<const V4a *>(p);
-#endif
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
   V4a u = {v.x, v.y, v.z, v.w};
-#if GCM_NT & 2
-  __builtin_nontemporal_store(u, reinterpret_cast<V4a *>(p));
-#else
   *reinterpret_cast<V4a *>(p) = u;
-#endif
 }
 __device__ __forceinline__ void st8(uint8_t *p, uint32_t a, uint32_t b) {
   V2a u = {a, b};
   *reinterpret_cast<V2a *>(p) = u;
-}
-
-// LDS writes at an explicit LDS byte address; ds_w128 at 4-byte alignment
-// relies on the unaligned LDS mode (tools/ldsalign.hip checks it on the
-// device), which the compiler does not assume: it would split the access.
-__device__ __forceinline__ void ds_w128(uint32_t addr, uint4 v) {
-  typedef uint32_t V4 __attribute__((ext_vector_type(4)));
-  const V4 u = {v.x, v.y, v.z, v.w};
-  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(u) : "memory");
-}
-__device__ __forceinline__ void ds_w32(uint32_t addr, uint32_t v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
-}
-// the ring's block writes: one ds_write_b128 (GCM_RING 1) or four dword
-// writes (GCM_RING 2)
-__device__ __forceinline__ void ring_w16(uint32_t addr, uint4 v) {
-#if GCM_RING == 2
-  asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %0, %2 offset:4\n\tds_write_b32 %0, %3 offset:8\n\tds_write_b32 %0, %4 offset:12"
-               ::"v"(addr), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w) : "memory");
-#else
-  ds_w128(addr, v);
-#endif
 }
 
 // Keep the first `rem` bytes of a 16-byte block, zero the rest.  Valid ESP
@@ -289,9 +171,9 @@ __device__ __forceinline__ void aes_round(uint32_t &s0, uint32_t &s1, uint32_t &
 // tools/gcm_timing.py --opts, bench.py --tuning gcm_opts=N): bit0 skips the
 // record loads and plaintext stores, bit1 the GHASH multiplies, bit2 the AES
 // rounds after round 2, bit3 the stores only, bit4 the loads only, bit5 the
-// per-session GHASH table staging, bit6 the per-record final multiply; bitsliced ctr pass: bit7 the AES
-// rounds but the last, bit8 the memory side (DMA, stores), bit9 the transposes.  They break results on purpose, to split
-// the kernel's time between memory, GHASH, AES and per-session setup.
+// per-session GHASH table staging, bit6 the per-record final multiply.  They
+// break results on purpose, to split the kernel's time between memory, GHASH,
+// AES and per-session setup.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t g_opts;
 __device__ __forceinline__ uint32_t gopts() {
@@ -496,143 +378,6 @@ __device__ __forceinline__ void aes_ctr2(const CtrCache &cc, uint32_t ca, uint32
   }
 }
 
-// ---- quad-bitsliced AES-CTR on the VALU (GCM_HYBRID) ------------------------
-// The T-table rounds cost the LDS pipe 16 lookups per block-round; bitsliced
-// rounds cost only VALU issue, which the T-table kernel leaves two-thirds idle.
-// The 4 lanes of a record (a quad) encrypt the 8 counter blocks of one pair
-// step together: lane q holds row q of the 8 states as 8 bit planes (bit
-// 8c + b of plane i = bit i of state byte (q, c) of block b), so a lane's
-// S-box is aes_bs.h's circuit on 8 registers (S' = S ^ 0x63, the round keys
-// are DevSA::dk's K_r ^ 0x63..), ShiftRows rotates each plane right by 8q,
-// and MixColumns takes rows q+1 and q+2 from the other lanes of the quad by
-// DPP quad_perm (the VALU's own operand crossbar: no LDS).  Round keys are
-// bit planes in LDS (2 ds_read_b128 per lane and round for 8 blocks).  The
-// keystream leaves as the T-table path's: lane q gets blocks q and q + 4 (AES
-// slots 4a + q and 4a + 4 + q) as memory-order words.  Host model, checked
-// against the table AES: tools/bsq_selftest.cpp.
-template <int CTRL>
-__device__ __forceinline__ uint32_t qperm(uint32_t x) {
-  // (bound_ctrl on: quad_perm never reads outside the quad, and it lets the
-  // DPP move fold into the consuming VALU instruction)
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
-}
-constexpr int kQpRot1 = 0x39;   // quad_perm [1,2,3,0]: lane q reads lane q+1
-constexpr int kQpXor2 = 0x4E;   // quad_perm [2,3,0,1]: lane q reads lane q^2 (= q+2)
-constexpr int kQpXor1 = 0xB1;   // quad_perm [1,0,3,2]: lane q reads lane q^1
-
-// bit i (within each byte) of a[s] <- bit s of a[i]: planes <-> per-block words
-__device__ __forceinline__ void bsq_transpose8(uint32_t (&a)[8]) {
-  constexpr uint32_t M[3] = {0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int j = 4 >> q;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k & j) continue;
-      const uint32_t t = __builtin_amdgcn_bitop3_b32(a[k] >> j, a[k + j], M[q], 0x28);   // (x ^ y) & m
-      a[k + j] ^= t;
-      a[k] ^= t << j;
-    }
-  }
-}
-
-// The session's round keys 1..10 as bit planes into LDS (at a session change):
-// word [r-1][q][i], byte c = bit i of key byte (q, c) of K'_r = byte q of dk[4r + c].
-template <int WG>
-__device__ __forceinline__ void stage_kp(uint8_t *dst, rkptr dk, int tid) {
-  for (int t = tid; t < 320; t += WG) {
-    const int r = (t >> 5) + 1, q = (t >> 3) & 3, i = t & 7;
-    uint32_t w = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) w |= (((dk[4 * r + c] >> (8 * q + i)) & 1u) * 0xffu) << (8 * c);
-    reinterpret_cast<uint32_t *>(dst)[t] = w;
-  }
-}
-
-// E_K(nonce || ctr0 + b), b = 0..7, AES-128: ka = block q, kb = block q + 4.
-// R: the lane's row of the three nonce columns entering round 1 (byte c =
-// state byte (q, c), c < 3; bswap'd s0c..s2c); rk3: round-0 key word of
-// column 3 (big-endian); qs = 8q; qb0 / qb1: bits 0 / 1 of q.  Every lane of
-// the wave must be active (DPP reads the quad's other lanes).
-__device__ __forceinline__ void aes_ctr8_bsq(uint32_t R, uint32_t ctr0, uint32_t rk3, uint32_t qs, bool qb0,
-                                             bool qb1, const uint8_t *lds, uint4 &ka, uint4 &kb) {
-  // VALU-only work: issue priority below the T-table steps of the other
-  // waves, whose lookups keep the LDS pipe busy (GCM_HYBRID_PRIO)
-  if (GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(0);
-  uint32_t P[8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) P[b] = R | ((((ctr0 + (uint32_t)b) ^ rk3) << qs) & 0xff000000u);
-  bsq_transpose8(P);
-  const uint8_t *kp = lds + LDS_KP + qs * 4;            // row q's planes of round 1
-#pragma unroll 1
-  for (int r = 0; r < 10; ++r) {
-    bs::sbox(P, 0u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) P[i] = __builtin_amdgcn_alignbit(P[i], P[i], qs);   // ShiftRows
-    if (r < 9) {
-      // out_q = xtime(s_q ^ s_q+1) ^ (s_q ^ s_q+1 ^ s_q+2 ^ s_q+3) ^ s_q
-      uint32_t t[8], u[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = P[i] ^ qperm<kQpRot1>(P[i]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) u[i] = t[i] ^ qperm<kQpXor2>(t[i]);
-      const uint32_t h = t[7];
-      P[0] = bs::x3(h, u[0], P[0]);
-      P[1] = bs::x3(bs::x3(t[0], h, u[1]), P[1], 0u);
-      P[2] = bs::x3(t[1], u[2], P[2]);
-      P[3] = bs::x3(bs::x3(t[2], h, u[3]), P[3], 0u);
-      P[4] = bs::x3(bs::x3(t[3], h, u[4]), P[4], 0u);
-      P[5] = bs::x3(t[4], u[5], P[5]);
-      P[6] = bs::x3(t[5], u[6], P[6]);
-      P[7] = bs::x3(t[6], u[7], P[7]);
-    }
-    const uint4 k0 = *reinterpret_cast<const uint4 *>(kp + r * 128);
-    const uint4 k1 = *reinterpret_cast<const uint4 *>(kp + r * 128 + 16);
-    P[0] ^= k0.x, P[1] ^= k0.y, P[2] ^= k0.z, P[3] ^= k0.w;
-    P[4] ^= k1.x, P[5] ^= k1.y, P[6] ^= k1.z, P[7] ^= k1.w;
-  }
-  bsq_transpose8(P);                                   // P[b]: byte c = keystream byte (q, c) of block b
-  // 4x4 word transposes across the quad (blocks 0..3 and 4..7): lane q then
-  // holds rows 0..3 of blocks q and q + 4
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      if (b & 2) continue;
-      const int x0 = 4 * h + b, x1 = x0 + 2;
-      const uint32_t y = qperm<kQpXor2>(qb1 ? P[x0] : P[x1]);
-      P[x0] = qb1 ? y : P[x0];
-      P[x1] = qb1 ? P[x1] : y;
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      if (b & 1) continue;
-      const int x0 = 4 * h + b, x1 = x0 + 1;
-      const uint32_t y = qperm<kQpXor1>(qb0 ? P[x0] : P[x1]);
-      P[x0] = qb0 ? y : P[x0];
-      P[x1] = qb0 ? P[x1] : y;
-    }
-  }
-  // rows -> memory-order column words
-  uint32_t C[8];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t *X = P + 4 * h;
-    const uint32_t T0 = perm(X[1], X[0], 0x05010400u), T1 = perm(X[1], X[0], 0x07030602u);
-    const uint32_t T2 = perm(X[3], X[2], 0x05010400u), T3 = perm(X[3], X[2], 0x07030602u);
-    C[4 * h + 0] = perm(T2, T0, 0x05040100u);
-    C[4 * h + 1] = perm(T2, T0, 0x07060302u);
-    C[4 * h + 2] = perm(T3, T1, 0x05040100u);
-    C[4 * h + 3] = perm(T3, T1, 0x07060302u);
-  }
-  ka = make_uint4(C[0], C[1], C[2], C[3]);
-  kb = make_uint4(C[4], C[5], C[6], C[7]);
-  if (GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(1);
-}
-
 // ---- GHASH multiply by a fixed power (gf_mul, gfmult.c:219-229) ----------
 // Y * H^S with 8-bit tables in LDS: 16 lookups, one per byte position p, of the
 // 16-byte product (the block whose byte p is v) * H^S, XOR-accumulated.
@@ -723,29 +468,6 @@ __device__ __forceinline__ uint4 gf_mul8_wide(uint4 x, const uint8_t *lds, const
   return make_uint4(r0, r1, r2, r3);
 }
 
-// Y * H^e with a 4-bit table in LDS at `base`, value-major (value n, nibble
-// position j at n*512 + j*16: GCM_FMUL_LDS).  Lane L walks the positions of
-// each half in the order t ^ (L & 15), so the 16 lanes of a ds_read_b128 group
-// read 16 different bank quads whatever their values.
-__device__ __forceinline__ uint4 gf_mul4_lds(uint4 x, const uint8_t *lds, uint32_t base, int lane) {
-  const uint32_t lm = (uint32_t)lane & 15u;
-  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-#pragma unroll 2
-  for (int t = 0; t < 16; ++t) {
-    const uint32_t q = (uint32_t)t ^ lm;
-    const uint32_t sh = (q & 7u) * 4u;
-    const uint32_t wl = (q & 8u) ? x.y : x.x, wh = (q & 8u) ? x.w : x.z;
-    const uint4 e = *reinterpret_cast<const uint4 *>(lds + base + ((wl >> sh) & 15u) * 512u + q * 16u);
-    const uint4 f = *reinterpret_cast<const uint4 *>(lds + base + ((wh >> sh) & 15u) * 512u + (16u + q) * 16u);
-    r0 = xor3(r0, e.x, f.x);
-    r1 = xor3(r1, e.y, f.y);
-    r2 = xor3(r2, e.z, f.z);
-    r3 = xor3(r3, e.w, f.w);
-    asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
-  }
-  return make_uint4(r0, r1, r2, r3);
-}
-
 // Y * H^e with the 4-bit table of that power in global memory (t = its 8 KiB:
 // nibble position j (byte j>>1, low nibble if j even), value n at j*256+n*16).
 // Used once per record per lane (the final x H^(8-l)), where the power differs
@@ -789,32 +511,16 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 
-// The Horner multiplier's 8-bit table (value-major, entry (v, q) at v*256 +
-// q*16) built in LDS from the same power's 4-bit table in gtab (nibble
-// position j, value n at j*256 + n*16; host_crypto.cpp ghash_tables).  The
-// multiply is GF(2)-linear in the block, so T8[v][q] = T4[2q][v & 15] ^
-// T4[2q+1][v >> 4]: a workgroup that changes session reads 8 KiB (which the
-// final multiply's gathers share) instead of copying the 64-KiB table.  The
-// reference precomputes its tables once per key (gmac.c:48-63 -> gfmult.c:87
-// gf128_genmultable4); here the 8-bit expansion is redone per workgroup.
-template <int WG>
-__device__ GCM_STAGE_INL void stage_h8(uint8_t *dst, const uint8_t *t4, int tid) {
-#pragma unroll 1     // (unrolled, the allocator spills more in the record loop)
-  for (int k = 0; k < (4096 + WG - 1) / WG; ++k) {
-    const int e = tid + k * WG;
-    if (4096 % WG == 0 || e < 4096) {
-      const int q = e & 15, v = e >> 4;
-      const uint4 lo = *reinterpret_cast<const uint4 *>(t4 + (2 * q) * 256 + (v & 15) * 16);
-      const uint4 hi = *reinterpret_cast<const uint4 *>(t4 + (2 * q + 1) * 256 + (v >> 4) * 16);
-      *reinterpret_cast<uint4 *>(dst + e * 16) = xor4(lo, hi);
-    }
-  }
-}
+// The cold work of the chunk loop (session-change table staging, the first
+// T-table fill, MODE 3's rollback of a failed record) runs as real calls:
+// kept out of the record loop's register allocation (gcm_kernel<3,1024,4>:
+// 16 -> 0 VGPRs spilled).
+#define GCM_COLD __noinline__
 
 // The Te0/Te1 pair table, 32 replicas, into LDS (a workgroup's first AEAD
 // chunk; out of line like the table staging)
 template <int WG>
-__device__ GCM_STAGE_INL void fill_tp(uint8_t *lds, const uint2 *tpair, int tid) {
+__device__ GCM_COLD void fill_tp(uint8_t *lds, const uint2 *tpair, int tid) {
   for (int idx = tid; idx < 256 * 32; idx += WG) {
     const int x = idx >> 5, r = idx & 31;
     const uint2 t = tpair[x];
@@ -823,17 +529,24 @@ __device__ GCM_STAGE_INL void fill_tp(uint8_t *lds, const uint2 *tpair, int tid)
   }
 }
 
-// stage_h8 through LDS: the power's 8 KiB 4-bit table into `scratch` with
-// one coalesced 16-byte load per thread (one L2/HBM round trip instead of
-// stage_h8's four dependent ones per thread -- at a session change of every
-// chunk, as in cfg4, those round trips were the staging's cost), then the
-// 8-bit entries from LDS.  Entry slot e takes q = e & 15 and v = (e >> 4) +
-// 17q (mod 256), so a 16-lane group reads 16 different bank quads for the low
+// The Horner multiplier's 8-bit table (value-major, entry (v, q) at v*256 +
+// q*16) built in LDS from the same power's 4-bit table in gtab (nibble
+// position j, value n at j*256 + n*16; host_crypto.cpp ghash_tables).  The
+// multiply is GF(2)-linear in the block, so T8[v][q] = T4[2q][v & 15] ^
+// T4[2q+1][v >> 4]: a workgroup that changes session reads 8 KiB (which the
+// final multiply's gathers share) instead of copying the 64-KiB table.  The
+// reference precomputes its tables once per key (gmac.c:48-63 -> gfmult.c:87
+// gf128_genmultable4); here the 8-bit expansion is redone per workgroup.
+// The 8 KiB come into `scratch` with one coalesced 16-byte load per thread
+// (one L2/HBM round trip: at a session change of every chunk, as in cfg4,
+// four dependent ones per thread were the staging's cost), then the 8-bit
+// entries from LDS.  Entry slot e takes q = e & 15 and v = (e >> 4) + 17q
+// (mod 256), so a 16-lane group reads 16 different bank quads for the low
 // nibble's row, at most 2 lanes per quad for the high one, and writes 16
 // different quads.  Contains a barrier: call it workgroup-uniformly, after
 // the workgroup's last read of dst and scratch.
 template <int WG>
-__device__ GCM_STAGE_INL void stage_h8_lds(uint8_t *dst, const uint8_t *t4, int tid, uint8_t *scratch) {
+__device__ GCM_COLD void stage_h8_lds(uint8_t *dst, const uint8_t *t4, int tid, uint8_t *scratch) {
   for (int i = tid; i < (int)(kGhPowerBytes / 16); i += WG)
     reinterpret_cast<uint4 *>(scratch)[i] = reinterpret_cast<const uint4 *>(t4)[i];
   __syncthreads();
@@ -849,7 +562,7 @@ __device__ GCM_STAGE_INL void stage_h8_lds(uint8_t *dst, const uint8_t *t4, int 
   }
 }
 
-// In place, one pass (MODE 3, GCM_INPLACE_ONEPASS): a record whose tag
+// In place, one pass (MODE 3): a record whose tag
 // failed already holds plaintext; XORing the same keystream over it again
 // restores the ciphertext exactly, so the buffer ends as cryptosoft's
 // verify-first leaves it (cryptosoft.c:595-633: a failed record is not
@@ -859,7 +572,7 @@ __device__ GCM_STAGE_INL void stage_h8_lds(uint8_t *dst, const uint8_t *t4, int 
 // schedule's), and out of line, so the record loop does not hold registers
 // for it.  Every lane of the wave calls it (back: this lane's record).
 template <int S>
-__device__ GCM_STAGE_INL void gcm_rollback(uint8_t *rec, int nct, int ct_len, bool back, int l, uint32_t s0c,
+__device__ GCM_COLD void gcm_rollback(uint8_t *rec, int nct, int ct_len, bool back, int l, uint32_t s0c,
                                           uint32_t s1c, uint32_t s2c, rkptr rk, uint32_t rk3, int nr,
                                           const uint8_t *lds, uint32_t slot) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -879,18 +592,19 @@ __device__ GCM_STAGE_INL void gcm_rollback(uint8_t *rec, int nct, int ct_len, bo
   }
 }
 
-// ---- one 8-record group per wave -----------------------------------------------
-// MODE 0: decrypt, single pass, plaintext to p.out (out-of-place device staging)
+// ---- one record group per wave (64 / S records) --------------------------------
+// MODE 0: decrypt, single pass, plaintext to p.out (out of place)
 // MODE 1: encrypt in place + ICV
-// MODE 2: decrypt in place, verify first (pass 1 GHASH + tag, pass 2 CTR)
 // MODE 3: decrypt in place, verify first, in one pass: MODE 0 over the record
 //         itself, then a failed record's keystream XORed over it again
+// (the two-pass in-place form, GHASH + tag then CTR over the verified
+// records, measured 1.60-1.64 vs 1.39-1.46 ms on cfg1: DESIGN.md §3.1)
 // Steps m, m+1 of a lane run together: 2 independent AES blocks, then
-// GHASH as (Y*H^8 ^ B_m)*H^8 ^ B_m+1 with the 8-bit table.
-template <int MODE, int S, bool RING = false, bool FM = false, bool HB = false>
+// GHASH as (Y*H^S ^ B_m)*H^S ^ B_m+1 with the 8-bit table.
+template <int MODE, int S>
 __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
-                                         uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk,
-                                         bool fm = false) {
+                                         uint32_t sa, uint32_t sa_flags, uint32_t mlen, int nr, rkptr rk) {
+  static_assert(MODE == 0 || MODE == 1 || MODE == 3, "decrypt out of place, encrypt, decrypt in place");
   const int lane = threadIdx.x & 63;
   const int l = lane & (S - 1);
   const uint32_t slot = ((uint32_t)(lane & 31) * 4) | (LDS_TP & 0xff0000u);
@@ -934,28 +648,11 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     return;
   }
   const uint32_t rk3 = rk[3];
-  // GCM_HYBRID: the lane's row (q = l) of the nonce columns entering round 1
-  const uint32_t qs = 8u * (uint32_t)(lane & 3);
-  const bool qb0 = (lane & 1) != 0, qb1 = (lane & 2) != 0;
-  uint32_t Rq = 0;
-  if (HB) {
-    const uint32_t sh = 24u - qs;
-    Rq = ((s0c >> sh) & 0xffu) | (((s1c >> sh) & 0xffu) << 8) | (((s2c >> sh) & 0xffu) << 16);
-  }
-#if GCM_OUTALIGN
-  // layout probe (tools/outalign_ab.sh, bench.py --out-pad 40; cfg1's
-  // 1500-byte slots only, results land elsewhere): record k's plaintext at
-  // out + k*1536 + 128, so every 128-byte line is written whole
-  // (GCM_OUTALIGN - 1: extra bytes past the line start, to separate the
-  // 16-byte alignment of the stores from the line completion)
-  uint8_t *orec = (MODE == 0 ? p.out + ((size_t)(rec - p.arena) / 1500) * 1536 + 112 + (GCM_OUTALIGN - 1) : rec);
-#else
   // out of place: the record's own offset in out, or (packed output) slot di
   // of out_stride bytes; orec is where the record's header would be, the
   // plaintext starts 16 bytes after it
   uint8_t *orec = (MODE == 0 ? (p.out_stride ? p.out + (size_t)di * p.out_stride - 16 : p.out - p.arena + rec)
                              : rec);
-#endif
   CtrCache cc;
   cc.hi = -1;                                               // built on first use
 
@@ -967,94 +664,6 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
                              (uint32_t)ct_len);
   };
 
-  // Output ring (RING, aligned schedule): the plaintext leaves as whole
-  // 128-byte lines.  AES pair step a (a even) produces the record's window
-  // [64a, 64a + 128) of plaintext, lane l blocks 4a + l and 4a + 4 + l (window
-  // offsets 16l and 64 + 16l).  The record's 128-byte LDS buffer holds the
-  // line at P + 64a (P = plaintext start) by address mod 128: write phase 1
-  // puts the window's bytes of that line (positions [r, 128), r = P mod 128)
-  // beside the r bytes the previous step left at [0, r); the four lanes read
-  // the whole line back (two aligned ds_read_b128 each) and store it with
-  // aligned 16-byte stores, only the plaintext bytes of the record's first and
-  // last lines dword by dword; write phase 2 then puts the window's bytes of
-  // the next line at [0, r).  Bytes past the plaintext (the J0 slot, a partial
-  // last block, idle lanes) land only on positions that are never stored.
-  // Writes are ds_write_b128 at 4-byte alignment (the unaligned LDS mode of
-  // gfx950, tools/ldsalign.hip); the one block per record that crosses the
-  // line boundary goes dword by dword.  Record i of the wave reads its line's
-  // halves in swapped order when bit 1 of i is set, so every ds_read_b128 of
-  // the line is conflict-free (16-lane groups see 16 distinct bank quads).
-  // P, r and the buffer offset are recomputed where they are used, from
-  // registers the loop keeps anyway (rec, di, the lane id): held across the
-  // loop they would be spilled (the kernel is at its 128-VGPR cap)
-  auto ring_P = [&]() -> uint8_t * {
-    uintptr_t rv = (uintptr_t)rec;
-    uint32_t dv = di;
-    asm volatile("" : "+v"(rv), "+v"(dv));
-    return p.out_stride ? p.out + (size_t)dv * p.out_stride : (uint8_t *)rv + (p.out - p.arena) + 16;
-  };
-  auto ring_off = [&]() -> uint32_t {
-    uint32_t t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    return LDS_RING + (t >> 2) * 128u;   // S == 4
-  };
-  // the line at P + 64a: its two 16-byte chunks of this lane from the ring
-  // (ring_read), then to memory (ring_store), plaintext bytes only
-  auto ring_read = [&](uint4 &v0, uint4 &v1) {
-    const uint32_t ro = ring_off();
-    const uint32_t c0 = (16u * (uint32_t)l + (((uint32_t)lane >> 3) & 1u) * 64u) & 127u;
-    v0 = *reinterpret_cast<const uint4 *>(lds + ro + c0);
-    v1 = *reinterpret_cast<const uint4 *>(lds + ro + (c0 ^ 64u));
-  };
-  auto ring_store = [&](int a, uint4 v0, uint4 v1) {
-    if (!valid) return;
-    const uint32_t c0 = (16u * (uint32_t)l + (((uint32_t)lane >> 3) & 1u) * 64u) & 127u;
-    uint8_t *const P = ring_P();
-    uint8_t *const Lc = (uint8_t *)(((uintptr_t)P + 64u * (uint32_t)a) & ~(uintptr_t)127);
-    const int rel0 = (int)(Lc - P);                          // line start relative to P
-    auto put = [&](uint32_t c, uint4 v) {
-      const int lo = rel0 + (int)c;
-      if (lo >= 0 && lo + 16 <= ct_len) {
-        *reinterpret_cast<uint4 *>(Lc + c) = v;
-      } else if (lo + 16 > 0 && lo < ct_len) {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (lo + 4 * k >= 0 && lo + 4 * k < ct_len) reinterpret_cast<uint32_t *>(Lc + c)[k] = w[k];
-      }
-    };
-    put(c0, v0);
-    put(c0 ^ 64u, v1);
-  };
-  auto ring_step = [&](int a, uint4 Oa, uint4 Ob) {
-    const uint32_t rb = (uint32_t)(uintptr_t)(lds + ring_off());   // LDS address of the buffer
-    const uint32_t sa_ = ((uint32_t)(uintptr_t)ring_P() & 127u) + 16u * (uint32_t)l, sb_ = sa_ + 64u;
-    const bool sta = sa_ < 128u && sa_ + 16u > 128u, stb = sb_ < 128u && sb_ + 16u > 128u;
-    const bool st = sta || stb;
-    const uint4 X = sta ? Oa : Ob;
-    const uint32_t sx = sta ? sa_ : sb_;
-    // phase 1: the bytes of the current line
-    if (sa_ + 16u <= 128u) ring_w16(rb + sa_, Oa);
-    if (sb_ + 16u <= 128u) ring_w16(rb + sb_, Ob);
-    if (st) ds_w32(rb + sx, X.x);
-    if (st && sx <= 120u) ds_w32(rb + sx + 4u, X.y);
-    if (st && sx == 116u) ds_w32(rb + sx + 8u, X.z);
-    uint4 v0, v1;
-    ring_read(v0, v1);
-    // phase 2: the bytes of the next line (the reads above are served first:
-    // a wave's LDS instructions execute in order)
-    if (sa_ >= 128u) ring_w16(rb + sa_ - 128u, Oa);
-    if (sb_ >= 128u) ring_w16(rb + sb_ - 128u, Ob);
-    if (st) ds_w32(rb + sx + 12u - 128u, X.w);
-    if (st && sx >= 120u) ds_w32(rb + sx + 8u - 128u, X.z);
-    if (st && sx == 124u) ds_w32(rb + sx + 4u - 128u, X.y);
-    ring_store(a, v0, v1);
-  };
-  auto ring_line = [&](int a) {
-    uint4 v0, v1;
-    ring_read(v0, v1);
-    ring_store(a, v0, v1);
-  };
   // GHASH input block of GHASH index i (>= 1) given its ciphertext C and
   // keystream ks; stores the output block (MODE 0: plaintext, MODE 1: CT).
   auto block_in = [&](int i, bool has_ct, uint4 C, uint4 ks) -> uint4 {
@@ -1079,13 +688,6 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   };
 
   uint4 Y = make_uint4(0, 0, 0, 0), EJ0 = make_uint4(0, 0, 0, 0);
-  // Experiment (GCM_PREFETCH, off): the small-batch kernel issuing each
-  // interior pair's ciphertext load one pair ahead.  Measured equal on a
-  // 32-record burst (the lone wave is VALU-issue-bound, not load-bound) and
-  // it makes the S = 8 kernels spill.
-  constexpr bool PF = GCM_PREFETCH && S == kGcmLanesSmall;
-  uint4 pCa = make_uint4(0, 0, 0, 0), pCb = make_uint4(0, 0, 0, 0);
-  int pf_m = -1;                                            // step held in pCa / pCb
   // Aligned schedule (MODE 0 / 1, S = 4, every record of the wave with pad =
   // S - 1, i.e. nct + 1 a multiple of S, as 1500-byte packets are): the AES
   // work is decoupled from the GHASH positions.  GHASH is unchanged (block i
@@ -1096,7 +698,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   // S - 1 GHASH step a + 1 of lane l hashes exactly slot j of AES step a, so
   // the ciphertext a lane loaded (or, encrypting, produced) is hashed one step
   // later from its own registers.
-  const bool aligned = GCM_ALIGNED && MODE != 2 && S == kGcmLanesPerRec && __all(!valid || pad == S - 1);
+  const bool aligned = S == kGcmLanesPerRec && __all(!valid || pad == S - 1);
   int m = aligned ? Mw : 0;
   if (aligned) {
     const int Ma = valid ? M - 1 : 0;
@@ -1114,7 +716,7 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       }
       const int rem = ct_len - 16 * j;
       const uint4 o = xor4(C, ks);
-      if (!RING && !(gopts() & 9)) st_partial(orec + 16 + 16 * j, o, rem);
+      if (!(gopts() & 9)) st_partial(orec + 16 + 16 * j, o, rem);
       if (MODE == 0 || MODE == 3) note_trailer(j + 1, o, rem);
       return mask_block(MODE == 1 ? o : C, rem);
     };
@@ -1134,14 +736,9 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
             Cb = ld16(rec + 16 + 16 * jb);
           }
           uint4 ka, kb;
-          if (HB && nr == 10 && (a >> 1) % kHyb == kHyb - 1)                  // wave-uniform
-            aes_ctr8_bsq(Rq, (uint32_t)(S * a) + 2u, rk3, qs, qb0, qb1, lds, ka, kb);
-          else
-            aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+          aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
           const uint4 Oa = xor4(Ca, ka), Ob = xor4(Cb, kb);
-          if (RING) {
-            ring_step(a, Oa, Ob);
-          } else if (valid && !(gopts() & 9)) {
+          if (valid && !(gopts() & 9)) {
             st16(orec + 16 + 16 * ja, Oa);
             st16(orec + 16 + 16 * jb, Ob);
           }
@@ -1169,7 +766,6 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         kb = aes_ctr(cc, cb, rk3, nr, rk, lds, slot);
         if (a + 1 < Ma) Bb = slot_out(jb, Cb, kb);
       }
-      if (RING) ring_step(a, xor4(Ca, ka), xor4(Cb, kb));
       // GHASH steps a (block prev) and a + 1 (block Ba), each only if <= Ma
       const uint4 Ym = a == 0 ? prev : xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), prev);
       if (valid && a <= Ma) Y = Ym;
@@ -1182,15 +778,12 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
       const uint4 Yn = xor4((gopts() & 2) ? Y : gf_mul8(Y, lds, gl), prev);
       if (valid && Ma == Maw) Y = Yn;
     }
-    // the line the last window ended in
-    if (RING) ring_line((Maw + 1) & ~1);
   }
   while (m < Mw) {
     const int i = S * m + l - pad;
-    if (m + 1 < Mw && (MODE != 2 || m > 0)) {
+    if (m + 1 < Mw) {
       // The pair needs the counter cache valid for both blocks (i < 0 is
-      // front padding: J0's counter).  MODE 2's first step stays single: it
-      // computes E_K(J0) there while its pairs run no AES.
+      // front padding: J0's counter).
       const uint32_t ca = i >= 0 ? (uint32_t)i + 1 : 1u, cb = (uint32_t)(i + S) + 1;
       if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
       if (__all((int)(cb >> 8) == cc.hi)) {
@@ -1202,50 +795,25 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         // unmasked.  Most pairs of a record take this path.
         if (__all(!valid || (i >= 1 && 16 * ib < ct_len))) {
           uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
-          if (PF && pf_m == m) {
-            Ca = pCa;
-            Cb = pCb;
-          } else if (valid && !(gopts() & 17)) {
+          if (valid && !(gopts() & 17)) {
             Ca = ld16(rec + 16 * i);
             Cb = ld16(rec + 16 * ib);
           }
-          if (PF) {
-            // the next pair, if it is interior for this lane (in bounds): the
-            // next step takes the interior path only if it is for every lane
-            const int in = i + 2 * S, inb = in + S;
-            if (valid && 16 * inb < ct_len && !(gopts() & 17)) {
-              pCa = ld16(rec + 16 * in);
-              pCb = ld16(rec + 16 * inb);
-            }
-            pf_m = m + 2;
-          }
-          uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
-          if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+          uint4 ka, kb;
+          aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
           uint4 Ba = Ca, Bb = Cb;
           if (MODE == 1) {
             Ba = xor4(Ca, ka);
             Bb = xor4(Cb, kb);
           }
-#if !GCM_STORE_LATE
-          if (MODE != 2 && valid && !(gopts() & 9)) {
+          if (valid && !(gopts() & 9)) {
             st16(orec + 16 * i, MODE == 1 ? Ba : xor4(Ca, ka));
             st16(orec + 16 * ib, MODE == 1 ? Bb : xor4(Cb, kb));
           }
-#else
-          const uint4 Oa = MODE == 1 ? Ba : xor4(Ca, ka), Ob = MODE == 1 ? Bb : xor4(Cb, kb);
-#endif
           if (gopts() & 2)
             Y = xor4(xor4(Y, Ba), Bb);
           else
             Y = xor4(gf_mul8(xor4(gf_mul8(Y, lds, gl), Ba), lds, gl), Bb);
-#if GCM_STORE_LATE
-          // stores after the GHASH: its wait for this pair's ciphertext does
-          // not also wait for the stores (vmcnt counts both, in order)
-          if (MODE != 2 && valid && !(gopts() & 9)) {
-            st16(orec + 16 * i, Oa);
-            st16(orec + 16 * ib, Ob);
-          }
-#endif
           m += 2;
           continue;
         }
@@ -1253,8 +821,8 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
         uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
         if (hca && !(gopts() & 17)) Ca = ld16(rec + 16 * i);
         if (hcb && !(gopts() & 17)) Cb = ld16(rec + 16 * ib);
-        uint4 ka = make_uint4(0, 0, 0, 0), kb = make_uint4(0, 0, 0, 0);
-        if (MODE != 2) aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
+        uint4 ka, kb;
+        aes_ctr2(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
         uint4 Ba;
         if (valid && i == 0) {                                     // AAD block
           Ba = sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0);
@@ -1281,12 +849,11 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     uint4 C = make_uint4(0, 0, 0, 0);
     if (has_ct) C = ld16(rec + 16 * i);
     if ((int)(ctr >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ctr >> 8), rk, lds, slot);
-    uint4 ks = make_uint4(0, 0, 0, 0);
     if (m > 0) {
       const uint4 Yn = gf_mul8(Y, lds, gl);
       if (m < M) Y = Yn;
     }
-    if (MODE != 2 || i == 0) ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
+    const uint4 ks = aes_ctr(cc, ctr, rk3, nr, rk, lds, slot);
     uint4 B;
     if (valid && i == 0) {
       B = sep ? make_uint4(spi, esnh, sn, 0) : make_uint4(spi, sn, 0, 0);     // AAD block
@@ -1313,12 +880,13 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   }
   // X = sum_l Y_l * H^(8-l)  (power index 7-l)
   uint4 Z;
+  // (from LDS tables -- 24 KiB more per session -- measured +0.6 % on cfg4,
+  // -1.7 % on cfg2; in 2 or 4 round trips instead of 4, equal or slower:
+  // DESIGN.md §5.1, §6)
   if (gopts() & 64)
     Z = Y;
-  else if (FM && fm)
-    Z = l == 0 ? gf_mul8(Y, lds, gl) : gf_mul4_lds(Y, lds, LDS_FM + (uint32_t)(S - 1 - l) * kGhPowerBytes, lane);
   else
-    Z = gf_mul4_global<GCM_FMU>(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
+    Z = gf_mul4_global(Y, p.gtab + (size_t)sa * kGhTableBytes + (uint32_t)(S - 1 - l) * kGhPowerBytes);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1) Z = xor4(Z, shfl_xor4(Z, o));
   const uint4 ej0 = shfl4(EJ0, (lane & ~(S - 1)) | pad);
@@ -1336,44 +904,6 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
   }
   if (MODE == 3 && __any(valid && !ok))
     gcm_rollback<S>(rec, nct, ct_len, valid && !ok, l, s0c, s1c, s2c, rk, rk3, nr, lds, slot);
-  if (MODE == 2) {
-    // pass 2: CTR decrypt in place, only for authenticated records.  No GHASH
-    // here, so the CT blocks are dealt densely (lane l of step a: block
-    // S*a + l, no padding or length-block slots), two blocks per lane per
-    // step, each step's loads issued before its rounds.
-    const int run = valid && ok;
-    int Mr = run ? (nct + S - 1) / S : 0;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) Mr = max(Mr, __shfl_xor(Mr, o));
-    auto put = [&](int c, uint4 C, uint4 ks) {
-      if (run && c < nct) {
-        const uint4 pt = xor4(C, ks);
-        st_partial(rec + 16 + 16 * c, pt, ct_len - 16 * c);
-        note_trailer(c + 1, pt, ct_len - 16 * c);
-      }
-    };
-    for (int a = 0; a < Mr; a += 2) {
-      const int ca = S * a + l, cb = ca + S;
-      const bool two = a + 1 < Mr;                                   // wave-uniform
-      uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
-      if (run && ca < nct) Ca = ld16(rec + 16 + 16 * ca);
-      if (two && run && cb < nct) Cb = ld16(rec + 16 + 16 * cb);
-      const uint32_t ta = (uint32_t)ca + 2, tb = (uint32_t)cb + 2;
-      if ((int)(ta >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ta >> 8), rk, lds, slot);
-      if (two && __all((int)(tb >> 8) == cc.hi)) {
-        uint4 ka, kb;
-        aes_ctr2(cc, ta, tb, rk3, nr, rk, lds, slot, ka, kb);
-        put(ca, Ca, ka);
-        put(cb, Cb, kb);
-      } else {
-        put(ca, Ca, aes_ctr(cc, ta, rk3, nr, rk, lds, slot));
-        if (two) {
-          if ((int)(tb >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(tb >> 8), rk, lds, slot);
-          put(cb, Cb, aes_ctr(cc, tb, rk3, nr, rk, lds, slot));
-        }
-      }
-    }
-  }
   if (want_trl) {
     // exactly one lane of the record holds it: OR over the 8 lanes
 #pragma unroll
@@ -1384,29 +914,28 @@ __device__ __forceinline__ void do_group(const GcmParams &p, const uint8_t *lds,
     p.status[di] = !valid ? ESPGPU_EINVAL : (ok ? ESPGPU_OK : ESPGPU_EBADMSG);
 }
 
-// ---- split design: a CTR pass and a GHASH / tag pass --------------------------
-// The fused kernel above walks each record with S = 4 lanes (the GHASH Horner
-// chain needs few lanes per record), so 256 records per CU are in flight and
-// every store straddles lines.  The split design runs the two halves of GCM
-// with the mapping each one wants:
-//  * ctr pass: AES-CTR only, kCtrLanes = 16 lanes per record (4 records per
-//    wave, 64 per CU), each lane two counter blocks per step; 256-byte
-//    contiguous loads and stores per record per instruction.  It also writes
-//    E_K(J0) for the tag pass (p.ej0[record]) and the fused trailer word.
-//  * tag pass: GHASH only, S = 4 lanes per record as in the fused kernel, with
-//    the 8-bit H^4 table the only LDS table; T = GHASH ^ E_K(J0) from p.ej0.
-// decrypt out of place: ctr (DIR 0) then tag (verify: status; a failed
-// record's trailer word is zeroed); encrypt: ctr (DIR 1, in place) then tag
-// (writes the ICV); decrypt in place, verify first: ctr (DIR 3: E_K(J0)
-// only), tag, then ctr (DIR 2: only records whose status is 0).
-constexpr int kCtrLanes = 16;
+// ---- the burst design's two halves: a CTR pass and a GHASH / tag pass ----------
+// For latency (gcm_burst_kernel, gcm_door_kernel below) the halves of GCM run
+// side by side with the mapping each one wants:
+//  * ctr pass (ctr_group): AES-CTR only, kBurstCtrLanes = 32 lanes per
+//    record, three counter blocks per lane, all lookups of a round issued
+//    before the wave waits (W); it also writes E_K(J0) (p.ej0[record]) and the
+//    fused trailer word;
+//  * tag pass (tag_group): GHASH only, S = 8 lanes per record with the 8-bit
+//    H^8 table; T = GHASH ^ E_K(J0).
+// decrypt out of place: ctr (DIR 0) beside the hash, then tag_finish
+// (verify: status; a failed record's trailer word is zeroed); encrypt: ctr
+// (DIR 1, in place) then tag (writes the ICV).  (As a throughput design --
+// two kernels, 16 ctr lanes per record -- it measured 1.72-1.74 vs 1.50 ms on
+// cfg1, and with a bitsliced ctr pass 2.26 ms: DESIGN.md §6.)
 // Burst kernel (gcm_burst_kernel below): 512-thread workgroups, because two
 // waves per SIMD leave 256 VGPRs per lane (at 1024 threads the 128-VGPR cap
 // spilled 20-28) and a burst never needs the occupancy; its ctr pass runs 32
 // lanes per record on waves [0, kBurstCtrWaves), its hash pass the rest.
 constexpr int kBurstWG = 512, kBurstCtrLanes = 32, kBurstCtrWaves = 5;
+constexpr uint32_t kBurstChunk = 4;     // records per burst chunk (at least; spread over the CUs)
 
-template <int DIR, int S = kCtrLanes, bool W = false>
+template <int DIR, int S, bool W>
 __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds, uint32_t di, bool have,
                                           uint32_t sa, uint32_t mlen, int nr, rkptr rk, uint32_t tbase = 0) {
   const int lane = threadIdx.x & 63;
@@ -1420,12 +949,11 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
     const uint32_t len = dv.y & 0xffffu;
     ct_len = (int)len - 16 - (int)mlen;
     valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
-    if (DIR == 2 && valid) valid = p.status[di] == ESPGPU_OK;
     if (valid) {
       rec = p.arena + (size_t)dv.x * 4;
       const uint4 h = ld16(rec);
       nct = (ct_len + 15) >> 4;
-      K = DIR >= 3 ? 1 : (nct + S) / S;                    // J0 + nct blocks over S lanes
+      K = (nct + S) / S;                                   // J0 + nct blocks over S lanes
       s0c = bswap32(dv.w) ^ rk[0];
       s1c = bswap32(h.z) ^ rk[1];
       s2c = bswap32(h.w) ^ rk[2];
@@ -1435,7 +963,7 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) Kw = max(Kw, __shfl_xor(Kw, o));
   if (Kw == 0) return;
-  const bool want_trl = (DIR == 0 || DIR == 2 || DIR == 4) && p.trailer != nullptr;
+  const bool want_trl = DIR == 0 && p.trailer != nullptr;
   uint8_t *orec = DIR == 0 ? p.out - p.arena + rec : rec;
   const uint32_t rk3 = rk[3];
   CtrCache cc;
@@ -1444,31 +972,29 @@ __device__ __forceinline__ void ctr_group(const GcmParams &p, const uint8_t *lds
   auto emit = [&](int i, bool loaded, uint4 C, uint4 ks) {
     if (!valid) return;
     if (i == -1) {
-      if (DIR != 2) p.ej0[di] = ks;
+      p.ej0[di] = ks;
       return;
     }
     if (!loaded) return;
     const int rem = ct_len - 16 * i;
     const uint4 o = xor4(C, ks);
-    if (DIR != 4) st_partial(orec + 16 + 16 * i, o, rem);
+    st_partial(orec + 16 + 16 * i, o, rem);
     if (want_trl && i == nct - 1)
       p.trailer[di] = esp_trailer_word(rem >= 16 ? o.w : (rem > 8 ? o.z : (rem > 4 ? o.y : o.x)),
                                        (uint32_t)ct_len);
   };
   for (int k = 0; k < Kw; k += 2) {
-    // DIR 4 (pre pass of the concurrent bitsliced design): lane 0 E_K(J0),
-    // lane 1 the last ciphertext block (the trailer word), nothing stored
-    const int ia = DIR == 4 ? (l == 0 ? -1 : (l == 1 ? nct - 1 : -2)) : l - 1 + S * k, ib = ia + S;
+    const int ia = l - 1 + S * k, ib = ia + S;
     const bool two = k + 1 < Kw;                           // wave-uniform
-    const bool la = DIR != 3 && valid && ia >= 0 && ia < nct;
-    const bool lb = DIR != 3 && DIR != 4 && valid && two && ib < nct;
+    const bool la = valid && ia >= 0 && ia < nct;
+    const bool lb = valid && two && ib < nct;
     uint4 Ca = make_uint4(0, 0, 0, 0), Cb = make_uint4(0, 0, 0, 0);
     if (la) Ca = ld16(rec + 16 + 16 * ia);
     if (lb) Cb = ld16(rec + 16 + 16 * ib);
     const uint32_t ca = (uint32_t)(ia + 2), cb = (uint32_t)(ib + 2);
     if ((int)(ca >> 8) != cc.hi) ctr_cache_build(cc, s0c, s1c, s2c, (int)(ca >> 8), rk, lds, slot);
     uint4 ka, kb = make_uint4(0, 0, 0, 0);
-    if (!GCM_CTR_SINGLE && two && __all((int)(cb >> 8) == cc.hi)) {
+    if (two && __all((int)(cb >> 8) == cc.hi)) {
       aes_ctr2<W>(cc, ca, cb, rk3, nr, rk, lds, slot, ka, kb);
     } else {
       ka = aes_ctr<W>(cc, ca, rk3, nr, rk, lds, slot);
@@ -1641,95 +1167,6 @@ __device__ __forceinline__ void tag_finish(const GcmParams &p, uint32_t di, uint
   if (p.trailer && !(valid && ok)) p.trailer[di] = 0;
 }
 
-#ifdef ESPGPU_VARIANTS
-// Measured-slower designs, built only into the variants
-// library (make -C f-stack_amd variants): the split design's two kernels.
-// KIND 0: the ctr pass (S = kCtrLanes, T-table in LDS); KIND 1: the tag pass
-// (S lanes per record, the H^S GHASH table in LDS).  Chunks, tickets and the
-// non-AEAD chunk rule as gcm_kernel.
-template <int KIND, int DIR, int WG, int S>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(GCM_SPLIT_WPE)))
-void gcm_split_kernel(GcmParams p) {
-  constexpr int RPW = 64 / S;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[65536];
-  const int tid = threadIdx.x;
-  if (KIND == 0) {
-    for (int idx = tid; idx < 256 * 32; idx += WG) {
-      const int x = idx >> 5, r = idx & 31;
-      const uint2 t = p.tpair[x];
-      *reinterpret_cast<uint32_t *>(lds + x * 256 + r * 4) = t.x;
-      *reinterpret_cast<uint32_t *>(lds + x * 256 + 128 + r * 4) = t.y;
-    }
-  }
-  const bool implicit = (p.chunks == nullptr);
-  const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
-  uint32_t cur_sa = 0xffffffffu, nr = 0, flags = 0, mlen = 16, mode = 0;
-  const int wave = tid >> 6;
-  __shared__ uint32_t s_ticket[2];
-  for (uint32_t it = 0;; ++it) {
-    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
-    __syncthreads();
-    const uint32_t c = s_ticket[it & 1];
-    if (c >= nch) break;
-    uint32_t sa, start, count;
-    if (implicit) {
-      start = c * p.chunk;
-      count = min(p.chunk, p.n - start);
-      sa = p.desc[start].sa;
-    } else {
-      const Chunk ch = p.chunks[c];
-      sa = ch.sa;
-      start = ch.start;
-      count = ch.count;
-    }
-    sa = __builtin_amdgcn_readfirstlane(sa);
-    if (sa != cur_sa) {
-      __syncthreads();
-      if (sa < p.nsas) {
-        const DevSA *sp = p.sas + sa;
-        nr = sp->nr;
-        flags = sp->flags;
-        mlen = sp->mlen;
-        mode = sp->mode;
-        if (KIND == 1 && mode == ESPGPU_CSP_MODE_AEAD)
-          stage_h8<WG>(lds, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
-      } else {
-        mode = 0;
-      }
-      cur_sa = sa;
-      __syncthreads();
-    }
-    for (uint32_t sub = 0; sub < count; sub += (uint32_t)(WG / 64) * RPW) {
-      const uint32_t rl = sub + (uint32_t)wave * RPW + (uint32_t)((tid & 63) / S);
-      const bool have = rl < count;
-      const uint32_t pos = start + (have ? rl : 0);
-      const uint32_t di = p.order ? p.order[pos] : pos;
-      if (mode != ESPGPU_CSP_MODE_AEAD) {
-        // the tag pass owns the statuses: EINVAL unless the ETA kernel's record
-        if (KIND == 1 && have && (tid & (S - 1)) == 0) {
-          const uint32_t rsa = p.desc[di].sa;
-          const bool eta = rsa < p.nsas && p.sas[rsa].mode == ESPGPU_CSP_MODE_ETA;
-          if (!eta) {
-            p.status[di] = ESPGPU_EINVAL;
-            if (DIR == 0 && p.trailer) p.trailer[di] = 0;
-          }
-        }
-        continue;
-      }
-      if (KIND == 0)
-        ctr_group<DIR, S>(p, lds, di, have, sa, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
-      else
-        tag_group<DIR, S>(p, lds, di, have, sa, flags, mlen);
-    }
-  }
-  if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
-    atomicExch(&p.queue[0], 0u);
-    atomicExch(&p.queue[1], 0u);
-  }
-}
-
-#endif  // ESPGPU_VARIANTS
-
 // Self-staging prologue of one chunk (gcm_kernel<..., STAGE>): copies the
 // chunk's descriptors (p.hdesc -> p.desc) and records (p.xin) from host memory
 // through the mapping and keeps its result spans (p.xout) in LDS for the
@@ -1775,14 +1212,8 @@ template <int MODE, int WG, int S, bool STAGE = false>
 __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   static_assert(S == kGcmLanesPerRec || S == kGcmLanesSmall, "GHASH tables exist for these strides");
   constexpr int RPW = 64 / S;             // records per wave
-  // the output ring (do_group): the headline decrypt's shape only
-  constexpr bool RING = GCM_RING && MODE == 0 && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
-  constexpr bool FM = GCM_FMUL_LDS && !RING && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
-  constexpr bool HB = GCM_HYBRID > 0 && !RING && !FM && S == kGcmLanesPerRec && WG == 1024 && !STAGE;
-  constexpr uint32_t LDS_H4 = LDS_BYTES + (RING ? kRingBytes : 0) + (FM ? kFmBytes : 0) + (HB ? kKpBytes : 0);
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_H4 + (GCM_H4_LDS ? kGhPowerBytes : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALL];
   const int tid = threadIdx.x;
-  if (HB && GCM_HYBRID_PRIO) __builtin_amdgcn_s_setprio(1);
   GCM_PHASE(0, true);
   // The T-table (per entry 32 slots of Te0 then 32 slots of Te1, see tpa())
   // is filled with the first session's GHASH table: a workgroup that draws no
@@ -1799,17 +1230,14 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // balances the chip where a static split would leave most CUs idle.
   // s_ticket is double-buffered by iteration parity: slot it&1 is rewritten
   // only at it+2, after every thread passed iteration it+1's barrier.
-  // With the ring no LDS byte is left for it: the ticket goes through the
-  // first ring line (tid 0's own record, idle between groups) and a second
-  // barrier keeps it until every wave has read it.
-  __shared__ uint32_t s_ticket[RING ? 1 : 2];
+  // (Per-XCD ticket counters measured equal on cfg4 and 13 % slower on
+  // cfg2, whose largest-first order they break: DESIGN.md §6.)
+  __shared__ uint32_t s_ticket[2];
   __shared__ XferSpan s_xout[STAGE ? 2 * kChunkRecs : 1];
   for (uint32_t it = 0;; ++it) {
-    uint32_t *tk = RING ? reinterpret_cast<uint32_t *>(lds + LDS_RING) : s_ticket + (it & 1);
-    if (tid == 0) *tk = GCM_XCDQ2 ? xcd_ticket(p.queue, blockIdx.x & 7u, nch) : atomicAdd(&p.queue[0], 1u);
+    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
     __syncthreads();
-    const uint32_t c = *tk;
-    if (RING) __syncthreads();
+    const uint32_t c = s_ticket[it & 1];
     GCM_PHASE(2, it == 0);
     if (c >= nch) break;
     uint32_t sa, start, count;
@@ -1839,23 +1267,9 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
           tfilled = true;
           GCM_PHASE(1, true);
         }
-        if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32)) {
-          if (GCM_H4_LDS)
-            stage_h8_lds<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes,
-                             tid, lds + LDS_H4);
-          else
-            stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes, tid);
-          if (HB && nr == 10) stage_kp<WG>(lds + LDS_KP, (rkptr)(const void *)(p.sas[sa].dk), tid);
-          if (FM && !implicit) {
-            // H^1..H^3 (power index i = 0..2): position-major in gtab (j*256 +
-            // n*16), value-major here (n*512 + j*16)
-            const uint4 *pw = reinterpret_cast<const uint4 *>(p.gtab + (size_t)sa * kGhTableBytes);
-            for (int q = tid; q < (int)(kFmBytes / 16); q += WG) {
-              const int i = q >> 9, j = (q >> 4) & 31, nv = q & 15;
-              *reinterpret_cast<uint4 *>(lds + LDS_FM + i * kGhPowerBytes + nv * 512 + j * 16) = pw[q];
-            }
-          }
-        }
+        if (mode == ESPGPU_CSP_MODE_AEAD && !(gopts() & 32))
+          stage_h8_lds<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + (size_t)(S - 1) * kGhPowerBytes,
+                           tid, lds + LDS_BYTES);
       } else {
         mode = 0;
       }
@@ -1885,8 +1299,7 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
         }
         continue;
       }
-      do_group<MODE, S, RING, FM, HB>(p, lds, di, have, sa, flags, mlen, (int)nr,
-                                      (rkptr)(const void *)(p.sas[sa].rk), !implicit);
+      do_group<MODE, S>(p, lds, di, have, sa, flags, mlen, (int)nr, (rkptr)(const void *)(p.sas[sa].rk));
     }
     GCM_PHASE(5, it == 0);
     if (STAGE) {
@@ -1913,7 +1326,6 @@ __global__ __launch_bounds__(WG) void gcm_kernel(GcmParams p) {
   // so once all have retired no ticket is drawn again: reset for the next launch.
   if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
     atomicExch(&p.queue[0], 0u);
-    if (GCM_XCDQ2) xcd_reset(p.queue);
     atomicExch(&p.queue[1], 0u);
   }
 }
@@ -1962,13 +1374,9 @@ __device__ __forceinline__ void burst_chunk(const GcmParams &p, uint8_t *lds, ui
       ss.flags = s->flags;
       ss.mlen = s->mlen;
       ss.mode = s->mode;
-      if (ss.mode == ESPGPU_CSP_MODE_AEAD) {  // H^8 (power index 7)
-        if (GCM_H4_LDS)
-          stage_h8_lds<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid,
-                           lds + LDS_BYTES);
-        else
-          stage_h8<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid);
-      }
+      if (ss.mode == ESPGPU_CSP_MODE_AEAD)    // H^8 (power index 7)
+        stage_h8_lds<WG>(lds + LDS_GT, p.gtab + (size_t)sa * kGhTableBytes + 7 * kGhPowerBytes, tid,
+                         lds + LDS_BYTES);
     } else {
       ss.mode = 0;
     }
@@ -2078,7 +1486,7 @@ template <int DIR, int WG, bool STAGE = false>
 __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
   [[maybe_unused]] constexpr int S = kGcmLanesSmall;    // for the phase clock
   GCM_PHASE(0, true);
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (GCM_H4_LDS ? kGhPowerBytes : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALL];
   const int tid = threadIdx.x;
   load_tpair<WG>(lds, p.tpair);
   GCM_PHASE(1, true);
@@ -2123,7 +1531,7 @@ __global__ __launch_bounds__(WG) void gcm_burst_kernel(GcmParams p) {
 // claim (poll() relaunches the kernel for a job published after that).
 template <int WG>
 __global__ __launch_bounds__(WG) void gcm_door_kernel(DoorArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES + (GCM_H4_LDS ? kGhPowerBytes : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALL];
   __shared__ uint4 s_z[kChunkRecs];
   __shared__ XferSpan s_xout[2 * kChunkRecs];
   __shared__ uint32_t s_cmd[2][4];                 // job, chunk, n, slot_op (double-buffered by parity)
@@ -2260,244 +1668,6 @@ __global__ __launch_bounds__(WG) void gcm_door_kernel(DoorArgs a) {
   }
 }
 
-#ifdef ESPGPU_VARIANTS
-// ---- bitsliced ctr pass (aes_bs.h) -------------------------------------------
-// The split design's ctr pass with the AES on the VALU instead of the LDS
-// (the T-table kernels are bound by the LDS lookup rate).  A
-// lane owns a WINDOW of 32 consecutive counters of one record (window w:
-// counters 32w .. 32w+31; CT block c has counter c + 2) and encrypts them
-// bitsliced, 32 blocks per register bit.  A chunk's windows are numbered by a
-// prefix sum over its records (a 1500-byte record has 3) and each thread takes
-// one.  After the rounds a 32x32 bit transpose per state word turns the
-// keystream into blocks, which the lane XORs into its own window's blocks.
-// The window's ciphertext comes into LDS by LDS-DMA (global_load_lds, no
-// VGPRs), a quarter (8 blocks) at a time in two buffers: quarters 0 and 1 are
-// requested before the rounds, so their latency hides under the AES; DMA
-// instruction k writes block k of every lane's window at k*1 KiB + lane*16,
-// which is also where the lane reads it back (conflict-free ds_read_b128).
-// DIR 0: decrypt out of place; SEQ: also E_K(J0) and the trailer word, for the
-//        tag pass that follows on the same stream (otherwise the concurrent
-//        design's pre pass, ctr_group<4>, writes them);
-// DIR 1: encrypt in place, E_K(J0) for the tag pass that follows;
-// DIR 2: decrypt in place the records whose status is OK (verify-first), with
-//        the trailer word.
-// Session keys: DevSA::dk of an AEAD session = K0, K'_1 .. K'_nr as
-// little-endian words with K'_r = K_r ^ 0x63..63 (aes_bs.h).
-constexpr int kBsWG = 256;                 // one wave per SIMD; two workgroups per CU
-constexpr uint32_t kBsQuarter = 8 * 64 * 16;   // LDS bytes of one quarter buffer (8 blocks x 64 windows)
-
-template <int DIR, bool SEQ>
-__global__ __launch_bounds__(kBsWG) __attribute__((amdgpu_waves_per_eu(2), amdgpu_num_vgpr(GCM_BS_VGPRS)))
-void gcm_bsctr_kernel(GcmParams p) {
-  constexpr int NW = kBsWG / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t s_ct[NW][2][kBsQuarter];   // ciphertext quarters, two buffers
-  __shared__ uint4 s_own[NW][64];     // the lane's window across the rounds: rec offset/4, ct_len, w, di
-  __shared__ uint32_t s_incl[kChunkRecs];
-  __shared__ uint32_t s_wsum[NW];
-  __shared__ uint32_t s_ticket[2];
-  static_assert(kChunkRecs == NW * 64, "one record per thread in the window scan");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS-DMA bases in SGPRs
-  const bool implicit = (p.chunks == nullptr);
-  const uint32_t nch = implicit ? (p.n + p.chunk - 1) / p.chunk : *p.nchunks;
-  const bool want_trl = (DIR == 2 || (DIR == 0 && SEQ)) && p.trailer != nullptr;
-  for (uint32_t it = 0;; ++it) {
-    if (tid == 0) s_ticket[it & 1] = atomicAdd(&p.queue[0], 1u);
-    __syncthreads();
-    const uint32_t c = s_ticket[it & 1];
-    if (c >= nch) break;
-    uint32_t sa, start, count;
-    if (implicit) {
-      start = c * p.chunk;
-      count = min(p.chunk, p.n - start);
-      sa = p.desc[start].sa;
-    } else {
-      const Chunk ch = p.chunks[c];
-      sa = ch.sa;
-      start = ch.start;
-      count = ch.count;
-    }
-    sa = __builtin_amdgcn_readfirstlane(sa);
-    const bool aead = sa < p.nsas && p.sas[sa].mode == ESPGPU_CSP_MODE_AEAD;
-    const uint32_t mlen = aead ? p.sas[sa].mlen : 16u;
-    // windows per record (0 for a record this pass does not touch; the tag
-    // pass owns every status)
-    uint32_t nw = 0;
-    if (aead && (uint32_t)tid < count) {
-      const uint32_t pos = start + (uint32_t)tid;
-      const uint32_t di = p.order ? p.order[pos] : pos;
-      const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
-      const uint32_t len = dv.y & 0xffffu;
-      const int ct_len = (int)len - 16 - (int)mlen;
-      bool valid = ((dv.y >> 16) == sa) && ct_len > 0 && (len & 3) == 0;
-      if (DIR == 2 && valid) valid = p.status[di] == ESPGPU_OK;
-      if (valid) nw = (((((uint32_t)ct_len + 15) >> 4) + 1) >> 5) + 1;   // counters 2 .. nct+1
-    }
-    uint32_t v = nw;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(v, o);
-      if (lane >= o) v += u;
-    }
-    if (lane == 63) s_wsum[wave] = v;
-    __syncthreads();
-    for (int k = 0; k < wave; ++k) v += s_wsum[k];
-    s_incl[tid] = v;
-    __syncthreads();
-    const uint32_t total = s_incl[kChunkRecs - 1];
-    const rkptr K = (rkptr)(const void *)(p.sas[aead ? sa : 0].dk);
-    const int nr = aead ? (int)p.sas[sa].nr : 0;
-    for (uint32_t base = 0; base < total; base += kBsWG) {
-      const uint32_t gw = base + (uint32_t)tid;
-      const bool has = gw < total;
-      if (!__any(has)) break;                         // wave-uniform: the tail pass
-      // owner record: the number of records whose inclusive count is <= gw
-      uint32_t r = 0;
-#pragma unroll
-      for (uint32_t step = kChunkRecs / 2; step; step >>= 1)
-        if (s_incl[r + step - 1] <= gw) r += step;
-      uint32_t di = 0, roff = 0, ctl = 0, w = 0, W0 = 0, W1 = 0, W2 = 0;
-      if (has) {
-        w = gw - (r ? s_incl[r - 1] : 0u);
-        const uint32_t pos = start + r;
-        di = p.order ? p.order[pos] : pos;
-        const uint4 dv = *reinterpret_cast<const uint4 *>(p.desc + di);
-        ctl = (dv.y & 0xffffu) - 16u - mlen;
-        roff = dv.x;
-        const uint4 h = ld16(p.arena + (size_t)roff * 4);
-        W0 = dv.w;                                    // salt
-        W1 = h.z;                                     // explicit IV
-        W2 = h.w;
-      }
-      // this lane's window: blocks cb = 32w + s - 2 of the record, s = 0..31;
-      // kept in LDS across the rounds (registers there hold the AES state)
-      s_own[wave][lane] = make_uint4(roff, has ? ctl : 0u, w, di);
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-      // Quarter buffer layout: window o's block k at o*128 + ((k - o) & 7)*16.
-      // In DMA / store instruction i, lanes 8m..8m+7 move window 8i + m's
-      // 128 contiguous bytes (block (j + o) & 7 on lane 8m + j, lane-linear in
-      // LDS at i*1 KiB + lane*16); the owner lane reads and writes its blocks
-      // across the 16 bank quads instead of one.
-      auto dma_quarter = [&](int q) {
-        uint8_t *buf = &s_ct[wave][q & 1][0];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int o = 8 * i + (lane >> 3);
-          const uint4 ow = s_own[wave][o];
-          const int cb = 32 * (int)ow.z + 8 * q + ((lane + o) & 7) - 2;
-          if (cb >= 0 && cb < (int)((ow.y + 15) >> 4))
-            __builtin_amdgcn_global_load_lds(p.arena + (size_t)ow.x * 4 + 16 + 16 * cb,
-                                             (__attribute__((address_space(3))) void *)(buf + i * 1024), 16, 0, 0);
-          if (i & 1) __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      if (!(gopts() & 256)) {
-        dma_quarter(0);
-        dma_quarter(1);
-      }
-      // bitsliced counter blocks salt || IV || BE32(32w + s), s = bit index
-      uint32_t st[128];
-      const uint32_t W3 = bswap32(32u * w);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t word = j < 4 ? W0 : j < 8 ? W1 : j < 12 ? W2 : W3;
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          st[8 * j + b] = (uint32_t)((int32_t)(word << (31 - (8 * (j & 3) + b))) >> 31);
-      }
-      st[120] = 0xAAAAAAAAu;                          // counter bits 0..4 = the slice
-      st[121] = 0xCCCCCCCCu;
-      st[122] = 0xF0F0F0F0u;
-      st[123] = 0xFF00FF00u;
-      st[124] = 0xFFFF0000u;
-#pragma unroll 1
-      for (int rr = 0; rr < ((gopts() & 128) ? 0 : nr - 1); ++rr) {
-        const uint32_t k[4] = {K[4 * rr], K[4 * rr + 1], K[4 * rr + 2], K[4 * rr + 3]};
-        bs::round<true>(st, k);
-      }
-      {
-        const uint32_t k[4] = {K[4 * nr - 4], K[4 * nr - 3], K[4 * nr - 2], K[4 * nr - 1]};
-        bs::round<false>(st, k);
-      }
-      // keystream blocks: word g of slice s -> st[32g + s], last round key added
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (!(gopts() & 512)) bs::transpose32(&st[32 * g]);
-        const uint32_t kl = K[4 * nr + g];
-#pragma unroll
-        for (int s = 0; s < 32; ++s) st[32 * g + s] ^= kl;
-      }
-      if (DIR == 1 || SEQ) {                          // slice 1 = counter 1 = J0
-        const uint4 o = s_own[wave][lane];
-        if (o.y != 0 && o.z == 0) p.ej0[o.w] = make_uint4(st[1], st[33], st[65], st[97]);
-      }
-      // quarters 0 and 1 (requested before the rounds), then 2 and 3 into the
-      // same two buffers once they are read
-      const uint4 own = s_own[wave][lane];
-      const uint32_t ctl2 = (gopts() & 256) ? 0u : own.y;
-      const int nct = (int)((ctl2 + 15) >> 4);
-      uint8_t *const obase = (DIR == 0 ? p.out : p.arena) + 16;
-      // rolled over the quarters: quarter q's keystream is always st[8 blocks
-      // at 32g .. 32g+7] and the state shifts down 8 blocks per quarter, so
-      // one loop body serves all four
-#pragma unroll 1
-      for (int q = 0; q < 4; ++q) {
-        if (q == 0 || q == 2) __builtin_amdgcn_s_waitcnt(0x0f70);          // vmcnt(0)
-        uint8_t *buf = &s_ct[wave][q & 1][0];
-        // owner: its 8 blocks of this quarter, ciphertext -> result in place
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int cb = 32 * (int)own.z + 8 * q + k - 2, sl = k;
-          if (cb >= 0 && cb < nct) {
-            uint4 *slot = reinterpret_cast<uint4 *>(buf + lane * 128 + ((k - lane) & 7) * 16);
-            const uint4 o4 = xor4(*slot, make_uint4(st[sl], st[32 + sl], st[64 + sl], st[96 + sl]));
-            *slot = o4;
-            const int rem = (int)ctl2 - 16 * cb;
-            if (want_trl && cb == nct - 1)
-              p.trailer[own.w] = esp_trailer_word(rem >= 16 ? o4.w : (rem > 8 ? o4.z : (rem > 4 ? o4.y : o4.x)), ctl2);
-          }
-          // one block at a time: hoisting the reads would hold them beside
-          // the 128 keystream registers
-          if (k & 1) __builtin_amdgcn_sched_barrier(0);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        // stores: 128 contiguous bytes per 8 lanes
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int o = 8 * i + (lane >> 3);
-          const uint4 ow = s_own[wave][o];
-          const int len = (gopts() & 256) ? 0 : (int)ow.y;
-          const int cb = 32 * (int)ow.z + 8 * q + ((lane + o) & 7) - 2;
-          if (cb >= 0 && cb < ((len + 15) >> 4))
-            st_partial(obase + (size_t)ow.x * 4 + 16 * cb, *reinterpret_cast<const uint4 *>(buf + i * 1024 + lane * 16),
-                       len - 16 * cb);
-          if (i & 1) __builtin_amdgcn_sched_barrier(0);
-        }
-        if (q == 1) {
-          // both buffers read (lgkmcnt 0) before the DMA overwrites them
-          __builtin_amdgcn_s_waitcnt(0xc07f);
-          dma_quarter(2);
-          dma_quarter(3);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int j = 0; j < 24; ++j) st[32 * g + j] = st[32 * g + j + 8];
-      }
-    }
-    // s_incl / s_own are rewritten by the next chunk
-    __syncthreads();
-  }
-  if (tid == 0 && atomicAdd(&p.queue[1], 1u) == gridDim.x - 1) {
-    atomicExch(&p.queue[0], 0u);
-    atomicExch(&p.queue[1], 0u);
-  }
-}
-
-#endif  // ESPGPU_VARIANTS
-
 }  // namespace
 
 #ifdef ESPGPU_KNOBS
@@ -2514,71 +1684,13 @@ int set_gcm_opts(uint32_t opts) {
 #endif
 }
 
-#ifdef ESPGPU_VARIANTS
-// The split design for a large batch (ctr and tag passes, see gcm_split_kernel):
-// kernels on one stream, each resetting its ticket counters before the next starts.
-static int launch_gcm_split(const GcmParams &p, int encrypt, int two_pass, int grid, hipStream_t st) {
-  constexpr int WG = 1024, S = kGcmLanesPerRec;
-  if (encrypt) {
-    hipLaunchKernelGGL((gcm_split_kernel<0, 1, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 1, WG, S>), dim3(grid), dim3(WG), 0, st, p);
-  } else if (two_pass) {
-    hipLaunchKernelGGL((gcm_split_kernel<0, 3, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
-    hipLaunchKernelGGL((gcm_split_kernel<0, 2, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
-  } else {
-    hipLaunchKernelGGL((gcm_split_kernel<0, 0, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// The bitsliced ctr pass (gcm_bsctr_kernel, its own ticket counters at
-// queue[4..5]) with the T-table tag pass.  bs.mode 1: one stream, ctr pass
-// then tag pass (the split design's order); bs.mode 2, decrypt out of place:
-// the ctr pass on `st` and, at the same time on bs.aux, the pre pass
-// (ctr_group<4>: E_K(J0) and the trailer word, two lanes per record) then the
-// tag pass, both in one-wave-per-SIMD workgroups so that they fit on every CU
-// beside the ctr pass's two (VALU-bound ctr waves and LDS-bound GHASH waves
-// share the CU); `st` waits for bs.aux before the batch completes.
-static int launch_gcm_bs(const GcmParams &p, int encrypt, int two_pass, int grid, hipStream_t st,
-                         const GcmBsLaunch &bs) {
-  constexpr int WG = 1024, S = kGcmLanesPerRec;
-  GcmParams pc = p;
-  pc.queue = p.queue + 4;
-  const int cgrid = 2 * grid;                                 // two ctr workgroups per CU
-  if (encrypt) {
-    hipLaunchKernelGGL((gcm_bsctr_kernel<1, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 1, WG, S>), dim3(grid), dim3(WG), 0, st, p);
-  } else if (two_pass) {
-    hipLaunchKernelGGL((gcm_split_kernel<0, 3, WG, kCtrLanes>), dim3(grid), dim3(WG), 0, st, p);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
-    hipLaunchKernelGGL((gcm_bsctr_kernel<2, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
-  } else if (bs.mode == 2 && bs.aux != nullptr) {
-    hipStream_t aux = reinterpret_cast<hipStream_t>(bs.aux);
-    hipEvent_t fork = reinterpret_cast<hipEvent_t>(bs.ev_fork), join = reinterpret_cast<hipEvent_t>(bs.ev_join);
-    if (hipEventRecord(fork, st) != hipSuccess || hipStreamWaitEvent(aux, fork, 0) != hipSuccess) return -1;
-    hipLaunchKernelGGL((gcm_bsctr_kernel<0, false>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
-    hipLaunchKernelGGL((gcm_split_kernel<0, 4, 256, 2>), dim3(grid), dim3(256), 0, aux, p);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 0, 256, S>), dim3(grid), dim3(256), 0, aux, p);
-    if (hipEventRecord(join, aux) != hipSuccess || hipStreamWaitEvent(st, join, 0) != hipSuccess) return -1;
-  } else {
-    hipLaunchKernelGGL((gcm_bsctr_kernel<0, true>), dim3(cgrid), dim3(kBsWG), 0, st, pc);
-    hipLaunchKernelGGL((gcm_split_kernel<1, 0, WG, S>), dim3(grid), dim3(WG), 0, st, p);
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-#endif  // ESPGPU_VARIANTS
-
 int launch_gcm_door(const DoorArgs &a, int grid, void *stream) {
   hipLaunchKernelGGL((gcm_door_kernel<kBurstWG>), dim3(grid), dim3(kBurstWG), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream,
-               const GcmBsLaunch *bs) {
+int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lanes, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
   constexpr int W = kGcmLanesSmall;
@@ -2596,21 +1708,11 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
   // burst kernel (small, E_K(J0) scratch given, out of place or encrypt):
   // chunks of one ctr wave's records, so a burst spreads over CUs
   const bool burst = small && pp.ej0 != nullptr && !two_pass;
-  const uint32_t rpw = burst ? 64 / kCtrLanes : 64 / (small ? W : kGcmLanesPerRec);
   const uint32_t per = (pp.n + (uint32_t)grid - 1) / (uint32_t)grid;
-  p.chunk = (small && !burst ? GCM_SMALL_CHUNK_WAVES : burst ? 1 : 4) * rpw;
+  p.chunk = burst ? kBurstChunk : small ? 64 / W : 4 * (64 / kGcmLanesPerRec);
   while (p.chunk < per && p.chunk < (uint32_t)kChunkRecs) p.chunk <<= 1;
-#if GCM_WG != 1024
-  if (!small) p.chunk = (GCM_WG / 64) * (64 / kGcmLanesPerRec);   // experiment: one pass per chunk
-#endif
   if (p.chunks == nullptr) grid = std::max(1, std::min(grid, (int)((p.n + p.chunk - 1) / p.chunk)));
-#ifdef ESPGPU_VARIANTS
-  if (!small && p.ej0 != nullptr && bs != nullptr && bs->mode) return launch_gcm_bs(p, encrypt, two_pass, grid, st, *bs);
-  if (!small && p.ej0 != nullptr) return launch_gcm_split(p, encrypt, two_pass, grid, st);
-#else
-  (void)bs;
-  if (!small && p.ej0 != nullptr) return -1;          // the split / bitsliced designs: variants build only
-#endif
+  if (!small && p.ej0 != nullptr) return -1;          // (the burst design serves small batches only)
   if (burst) {
     if (p.xin != nullptr && p.chunks != nullptr) return -1;   // self-staging: implicit chunks only
     if (p.xin != nullptr && encrypt)
@@ -2639,11 +1741,11 @@ int launch_gcm(const GcmParams &pp, int encrypt, int two_pass, int grid, int lan
     else
       hipLaunchKernelGGL((gcm_kernel<0, 1024, W>), dim3(grid), dim3(1024), 0, st, p);
   } else if (encrypt) {
-    hipLaunchKernelGGL((gcm_kernel<1, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<1, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
   } else if (two_pass) {
-    hipLaunchKernelGGL((gcm_kernel<kGcmInPlaceMode, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<kGcmInPlaceMode, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
   } else {
-    hipLaunchKernelGGL((gcm_kernel<0, GCM_WG, kGcmLanesPerRec>), dim3(grid), dim3(GCM_WG), 0, st, p);
+    hipLaunchKernelGGL((gcm_kernel<0, 1024, kGcmLanesPerRec>), dim3(grid), dim3(1024), 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -199,27 +199,10 @@ struct espgpu_ctx {
   int n_gcm = 0;                 // live AEAD (GCM) sessions
   bool plan_dirty = true;        // planner key counts not known to be zero (plan_scan re-zeroes them)
   int n_whash = 0;   // ETA sessions with HMAC-SHA2-384/512 (the wide-hash two-pass kernels)
-  // ETA decrypt kernels (launch_eta; set_tuning "eta_fused"): 2 (default) =
-  // out of place the verify-first two-pass kernel (MODE 3: HMAC lane = record,
-  // then the block-parallel decrypt of the verified records into out; cfg3
-  // 2.39-2.45 ms), in place MODE 2 (2.44 ms); 1 = out of place one fused pass
-  // per cipher (MODE 0, 2.53-2.55 ms); 0 = separate verify and decrypt
-  // kernels (2.52 / 2.55 ms); 3 = out of place the verify and decrypt passes
-  // interleaved in one loop per wave (MODE 7), in place as 2
-  int eta_fused = 2;
   // GCM lanes per record: 0 = by batch size, 4 or 8 forced (set_tuning
   // "gcm_lanes": the tests run both kernels at every batch size)
   int gcm_lanes = 0;
-  // GCM design for large batches (set_tuning "gcm_split"): 0 = the fused
-  // kernel, 1 = the ctr pass + tag pass (esp_gcm.hip gcm_split_kernel), which
-  // keep E_K(J0) per record in d_ej0
-  int gcm_split = 0;
-  // Bitsliced ctr pass for large batches (set_tuning "gcm_bs", esp_gcm.hip
-  // gcm_bsctr_kernel): 0 = off, 1 = ctr pass then tag pass, 2 = out-of-place
-  // decrypt with the tag pass concurrently on s_aux (fork/join events)
-  int gcm_bs = 0;
-  hipStream_t s_aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // E_K(J0) scratch of the burst kernel
   uint4 *d_ej0 = nullptr;
   uint32_t ej0_cap = 0;
   // planner workspace
@@ -758,13 +741,12 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     p.nchunks = c->d_nchunks;
   }
   const int two_pass = (!encrypt && p.out == d_arena);
-  // E_K(J0) scratch: the split design (large batches, set_tuning gcm_split) and
-  // the burst kernel (small batches of <= gcm_burst records, out of place or
-  // encrypt; launch_gcm picks the kernel from it)
+  // E_K(J0) scratch: the burst kernel (small batches of <= gcm_burst records,
+  // out of place or encrypt; launch_gcm picks the kernel from it)
   const bool gsmall = c->gcm_lanes ? c->gcm_lanes == kGcmLanesSmall : n < kGcmSmallBatch;
   // (packed output: the fused kernel only)
   if ((kinds & 1) && !out_stride &&
-      (((c->gcm_split || c->gcm_bs) && !gsmall) || (gsmall && !two_pass && n <= c->gcm_burst))) {
+      gsmall && !two_pass && n <= c->gcm_burst) {
     if (n > c->ej0_cap) {
       hipFree(c->d_ej0);
       c->d_ej0 = nullptr;
@@ -774,7 +756,6 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     }
     p.ej0 = c->d_ej0;
   }
-  const GcmBsLaunch bs{c->gcm_bs, c->s_aux, c->ev_fork, c->ev_join};
   // beside a running doorbell kernel (one workgroup per CU on door_wg CUs)
   // the other kernels take the remaining CUs: every workgroup of theirs must
   // run for the launch to finish
@@ -785,7 +766,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   // GCM records), but a few workgroups do: the others would only draw a
   // ticket past the end (cfg3: ~9 us -> ~3 us per batch)
   const int ggrid = c->n_gcm > 0 ? grid : std::min(grid, 16);
-  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, ggrid, c->gcm_lanes, st, &bs))
+  if ((kinds & 1) && launch_gcm(p, encrypt, two_pass, ggrid, c->gcm_lanes, st))
     return fail(c, ESPGPU_EIO, "GCM kernel launch failed");
   if ((kinds & 2) && c->n_eta > 0) {
     EtaParams q{};
@@ -806,10 +787,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     q.nsas = nsas;
     const int ek = (c->n_cbc > 0 ? 1 : 0) | (c->n_ctr > 0 ? 2 : 0) | (c->n_wcbc > 0 ? 4 : 0) |
                    (c->n_wctr > 0 ? 8 : 0) | (c->n_whash > 0 ? 16 : 0);
-    q.two_pass_all = c->eta_fused == 2 || c->eta_fused == 3;
-    q.interleave = c->eta_fused == 3;
-    const EtaAux eaux{c->s_aux, c->ev_fork, c->ev_join, c->d_queue + 2 * kQueueRegionWords};
-    if (launch_eta(q, encrypt, ek, grid, c->eta_fused, st, &eaux))
+    if (launch_eta(q, encrypt, ek, grid, st))
       return fail(c, ESPGPU_EIO, "ETA kernel launch failed");
   }
   HIPCHK(c, hipEventRecord(c->ev_last, st));
@@ -858,8 +836,7 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     if (hipSetDevice(cfg.device) != hipSuccess) { rc = fail(c, ESPGPU_ENODEV, "hipSetDevice failed"); break; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s_aux, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
       rc = fail(c, ESPGPU_EIO, "stream");
       break;
     }
@@ -870,8 +847,6 @@ int espgpu_init(const espgpu_config *cfg_in, espgpu_ctx **out) {
     hipEventCreate(&c->ev0);
     hipEventCreate(&c->ev1);
     hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming);
-    hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-    hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     c->ready.reserve((size_t)cfg.batch_records * cfg.nbatches + 1024);
     if (hipMalloc(&c->d_sas, (size_t)cfg.max_sessions * sizeof(DevSA)) != hipSuccess ||
         hipMalloc(&c->d_gtab, (size_t)cfg.max_sessions * kGhTableBytes) != hipSuccess ||
@@ -918,7 +893,7 @@ void espgpu_fini(espgpu_ctx *c) {
       if (now_ns() - t0 > (uint64_t)c->deadline_ms * 1000000ull) { idle = false; break; }
       sched_yield();
     }
-    for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux}) idle = stream_settle(c, st) && idle;
+    for (hipStream_t st : {c->s_in, c->stream, c->s_out}) idle = stream_settle(c, st) && idle;
     for (auto &s : c->slots) idle = stream_settle(c, s.st) && idle;
     if (!idle) {
       fprintf(stderr, "espgpu_fini: device work of a failed context never finished; its memory is leaked\n");
@@ -927,7 +902,7 @@ void espgpu_fini(espgpu_ctx *c) {
     }
   }
   door_free(c);
-  for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux})
+  for (hipStream_t st : {c->s_in, c->stream, c->s_out})
     if (st) hipStreamSynchronize(st);
   for (auto &s : c->slots) free_slot(s);
   for (const HostRegion &r : c->regions)
@@ -944,9 +919,7 @@ void espgpu_fini(espgpu_ctx *c) {
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->ev_last) hipEventDestroy(c->ev_last);
-  if (c->ev_fork) hipEventDestroy(c->ev_fork);
-  if (c->ev_join) hipEventDestroy(c->ev_join);
-  for (hipStream_t st : {c->s_in, c->stream, c->s_out, c->s_aux})
+  for (hipStream_t st : {c->s_in, c->stream, c->s_out})
     if (st) hipStreamDestroy(st);
   delete c;
 }
@@ -1364,8 +1337,8 @@ static int launch_slot(espgpu_ctx *c, Slot &s) {
   // registered memory) and the results back, reading the descriptors and
   // writing the statuses through the host mapping -- one launch per burst
   // instead of copy, kernel, copy (set_tuning "stage_fused"; the small-batch
-  // GCM kernel, so not with gcm_lanes 4 or gcm_split forced)
-  const bool one_gcm = !s.mixed && s.kinds == 1 && c->gcm_lanes != kGcmLanesPerRec && !c->gcm_split;
+  // GCM kernel, so not with gcm_lanes 4 forced)
+  const bool one_gcm = !s.mixed && s.kinds == 1 && c->gcm_lanes != kGcmLanesPerRec;
   // Doorbell path (set_tuning "door"): a single-session GCM batch of up to
   // gcm_burst records is published to the persistent kernel -- descriptors
   // and span lists at the slot's fixed door offsets, then one 16-byte job in
@@ -1882,27 +1855,6 @@ int espgpu_decrypt_host(espgpu_ctx *c, const uint8_t *h_arena, uint64_t arena_by
 int espgpu_set_tuning(espgpu_ctx *c, const char *key, int value) {
   if (!c || !key) return ESPGPU_EINVAL;
   if (!strcmp(key, "grid")) { c->cfg.grid = (uint32_t)value; return 0; }
-  // the measured-slower designs exist only in the variants
-  // library (make -C f-stack_amd variants): ENOTSUP here for anything but
-  // the default
-  if (!strcmp(key, "eta_fused")) {
-    if (value < 0 || value > 4) return ESPGPU_EINVAL;
-    if (!kVariants && value != 2) return ESPGPU_ENOTSUP;
-    c->eta_fused = value;
-    return 0;
-  }
-  if (!strcmp(key, "gcm_split")) {
-    if (value != 0 && value != 1) return ESPGPU_EINVAL;
-    if (!kVariants && value) return ESPGPU_ENOTSUP;
-    c->gcm_split = value;
-    return 0;
-  }
-  if (!strcmp(key, "gcm_bs")) {
-    if (value < 0 || value > 2) return ESPGPU_EINVAL;
-    if (!kVariants && value) return ESPGPU_ENOTSUP;
-    c->gcm_bs = value;
-    return 0;
-  }
   if (!strcmp(key, "gcm_lanes")) {
     if (value != 0 && value != kGcmLanesPerRec && value != kGcmLanesSmall) return ESPGPU_EINVAL;
     c->gcm_lanes = value;

@@ -12,9 +12,7 @@ namespace espgpu {
 // GCM: rk[] is the AES encryption schedule in "kernel form" for the pair-table
 //   round (esp_gcm.hip): rk[0..3] raw, rk[4r..4r+3] = ror16(rk) for the
 //   middle rounds, rk[4nr..] byte-swapped (the last round emits little-endian
-//   words); dk[] = the schedule for the bitsliced ctr pass (aes_bs.h): K0 and
-//   K_r ^ 0x63636363 (r >= 1) as little-endian words.  The GHASH tables live
-//   in a separate array.
+//   words); dk[] unused.  The GHASH tables live in a separate array.
 // ETA: rk[] = encryption schedule (raw, big-endian words, rijndael-alg-fst.c
 //   layout), dk[] = decryption schedule (rijndaelKeySetupDec layout), ipad/opad
 //   = SHA-1 chaining state after one block of key^0x36 / key^0x5c
@@ -45,13 +43,6 @@ static_assert(sizeof(DevSA) == 1024, "DevSA is 1 KiB");
 // its Horner multiplier H^S in LDS (esp_gcm.hip stage_h8: byte position p,
 // value v at v*256 + p*16, value-major so a row's 16 positions sit in the 16
 // bank quads; gf_mul8) whenever it changes session.
-// The measured-slower designs (GCM split / bitsliced, ETA MODE 0 / 5+6 / 7)
-// are compiled only into the variants library (-DESPGPU_VARIANTS).
-#ifdef ESPGPU_VARIANTS
-constexpr bool kVariants = true;
-#else
-constexpr bool kVariants = false;
-#endif
 constexpr int kGcmLanesPerRec = 4;                               // GCM kernel: lanes per record
 constexpr int kGcmLanesSmall = 8;                                // small batches: shorter serial chain
 constexpr uint32_t kGcmSmallBatch = 32768;                       // records: below, 8 lanes per record still fit the chip
@@ -89,7 +80,7 @@ struct GcmParams {
   uint32_t *queue;
   uint32_t *trailer;              // decrypt: fused esp_input_cb trailer words, or nullptr
   uint32_t chunk;                 // implicit mode: records per chunk (launch_gcm sets it)
-  uint4 *ej0;                     // split design: E_K(J0) per descriptor (nullptr: fused kernel)
+  uint4 *ej0;                     // burst design: E_K(J0) per descriptor (nullptr: fused kernel)
   // A small single-session process batch that stages its own records (one
   // kernel instead of copy, kernel, copy): per descriptor i, xin[i] copies the
   // record into the arena before its chunk runs and xout[2i], xout[2i+1] copy
@@ -106,32 +97,8 @@ struct GcmParams {
 };
 
 // Work-queue regions (ctx d_queue): one per kernel family, kQueueRegionWords
-// apart.  Word 0 = the single ticket counter, word 1 = retired count; with
-// per-XCD queues (xcd_ticket) the 8 counters sit at kQueueXcdStride * (x + 1),
-// 256 bytes apart.
+// apart.  Word 0 = the ticket counter, word 1 = retired count.
 constexpr uint32_t kQueueRegionWords = 1024;
-constexpr uint32_t kQueueXcdStride = 64;
-
-// Per-XCD tickets: a workgroup draws from the counter of its XCD (workgroups
-// are dispatched to the 8 XCDs round-robin: x = blockIdx.x & 7), ticket k of
-// counter x is unit x + 8k, so every XCD walks the same unit order (the
-// planner's largest first); a workgroup whose counter is exhausted tries the
-// other XCDs' in turn.  One device-scope counter serializes its atomics at
-// 12-14 ns each, eight at 2-2.4 ns (tools/atomicprobe.hip,
-// profiles/r5_eta_knobs_fm_atomics.txt).  Returns n when every counter is past
-// the end; the caller's last retiring workgroup / wave clears all eight.
-__device__ __forceinline__ uint32_t xcd_ticket(uint32_t *q, uint32_t x, uint32_t n) {
-  for (uint32_t j = 0; j < 8; ++j) {
-    const uint32_t xx = (x + j) & 7u;
-    const uint32_t k = atomicAdd(q + kQueueXcdStride * (xx + 1), 1u);
-    const uint32_t u = xx + 8u * k;
-    if (u < n) return u;
-  }
-  return n;
-}
-__device__ __forceinline__ void xcd_reset(uint32_t *q) {
-  for (uint32_t x = 0; x < 8; ++x) atomicExch(q + kQueueXcdStride * (x + 1), 0u);
-}
 
 struct EtaParams {
   uint8_t *arena;
@@ -149,9 +116,6 @@ struct EtaParams {
   const uint8_t *isbox;           // inverse S-box (256 B)
   uint8_t *status;
   uint32_t nsas;
-  uint32_t two_pass_all;           // out of place: MODE 3 serves every ETA session (eta_fused 2)
-  uint32_t interleave;             // out of place: MODE 7 (verify and decrypt interleaved) instead of MODE 3's
-                                   // SHA-1 / SHA2-256 launch (eta_fused 3)
 };
 
 // esp_input_cb's checks on the last 3 plaintext bytes (xform_esp.c:597-630),
@@ -236,28 +200,13 @@ struct DoorArgs {
 int launch_gcm_door(const DoorArgs &a, int grid, void *stream);
 // lanes: 0 = by batch size (kGcmLanesSmall below kGcmSmallBatch records,
 // else kGcmLanesPerRec), or force 4 / 8 (set_tuning "gcm_lanes", tests)
-// The bitsliced ctr pass for large batches (set_tuning "gcm_bs"): mode 0 off,
-// 1 ctr pass then tag pass on the stream, 2 out-of-place decrypt with the tag
-// pass on `aux` concurrently (ev_fork / ev_join order it against the stream).
-struct GcmBsLaunch {
-  int mode;
-  void *aux, *ev_fork, *ev_join;
-};
-int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int lanes, void *stream,
-               const GcmBsLaunch *bs = nullptr);
-int set_gcm_opts(uint32_t opts);   // measurement knobs (KNOBS=1 builds only)
+int launch_gcm(const GcmParams &p, int encrypt, int two_pass, int grid, int lanes, void *stream);
+int set_gcm_opts(uint32_t opts);   // measurement knobs (`make knobs` builds only)
 int set_eta_opts(uint32_t opts);
-// kinds (decrypt): bit 0 = CBC sessions in the SA table, bit 1 = CTR ones
-// fused: 1 = the one-pass out-of-place decrypt (MODE 0) / verify-first
-// in-place kernel (MODE 2); 0 = verify pass + block-parallel decrypt pass
-// the concurrent ETA design's second stream (eta_fused 4): its own work
-// queue words, fork / join events
-struct EtaAux {
-  void *aux, *ev_fork, *ev_join;
-  uint32_t *queue;
-};
-int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, int fused, void *stream,
-               const EtaAux *aux = nullptr);
+// kinds: bit 0 = SHA-1 / SHA2-256 / no-auth CBC sessions in the SA table,
+// bit 1 = such CTR (or ESP-NULL) ones, bits 2 / 3 = SHA2-384/512 CBC / CTR
+// ones, bit 4 = any SHA2-384/512 session
+int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream);
 int launch_replay_check(const uint8_t *arena, espgpu_desc *desc, uint32_t n, const espgpu_replay *rp,
                         uint32_t nrp, const uint32_t *bitmap, uint8_t *rstatus, void *stream);
 int launch_xfer(const XferSpan *spans, uint32_t nspans, const uint8_t *status, void *stream);

@@ -15,14 +15,6 @@ for p in (os.path.join(ROOT, "f-stack_amd"), os.path.join(ROOT, "oracle"), ROOT)
     if p not in sys.path:
         sys.path.insert(0, p)
 
-# ESPGPU_VARIANTS=1: run the suite on libespgpu_variants.so, the engine plus
-# the measured-slower designs (GCM split / bitsliced passes, ETA MODE 0 /
-# 5+6 / 7), and add them to the parametrized GCM and ETA tests.
-# The default suite runs the shipped library's kernels only.
-VARIANTS = os.environ.get("ESPGPU_VARIANTS") == "1"
-if VARIANTS:
-    os.environ["ESPGPU_LIB"] = os.path.join(ROOT, "f-stack_amd", "libespgpu_variants.so")
-variants_only = pytest.mark.skipif(not VARIANTS, reason="variants library only (ESPGPU_VARIANTS=1)")
 
 
 def _make(args, fatal=True):
@@ -42,13 +34,9 @@ def pytest_configure(config):
     if os.path.isdir("/root/reference/freebsd"):
         _make(["-C", "oracle", "ref"], fatal=False)
     _make(["-C", "f-stack_amd", "-j8"])
-    if VARIANTS:
-        _make(["-C", "f-stack_amd", "-j8", "variants"])
 
 
-_GCM_DESIGNS = [((4, 0, 0, 0), "lanes4"), ((8, 0, 0, 0), "lanes8"), ((8, 0, 1 << 30, 0), "burst")]
-if VARIANTS:
-    _GCM_DESIGNS += [((4, 1, 0, 0), "split"), ((4, 0, 0, 1), "bs"), ((4, 0, 0, 2), "bsconc")]
+_GCM_DESIGNS = [((4, 0), "lanes4"), ((8, 0), "lanes8"), ((8, 1 << 30), "burst")]
 
 
 @pytest.fixture(params=[d for d, _ in _GCM_DESIGNS], ids=[i for _, i in _GCM_DESIGNS])
@@ -56,21 +44,13 @@ def gcm_lanes(request, drv):
     """Run a GCM test through every shipped GCM kernel design whatever its
     batch size: the fused kernel with 4 lanes per record (throughput) and
     with 8 (small batches, half the serial steps), and the burst kernel (both
-    passes in one launch; decrypt in place keeps the fused kernel).  With
-    ESPGPU_VARIANTS=1 also the measured-slower designs: the split design (a
-    CTR pass then a GHASH / tag pass) and the bitsliced ctr pass with the tag
-    pass after it (bs) or, decrypting out of place, beside it on a second
-    stream (bsconc).  set_tuning "gcm_lanes" / "gcm_split" / "gcm_burst" /
-    "gcm_bs", reset afterwards."""
-    lanes, split, burst, bs = request.param
+    passes in one launch; decrypt in place keeps the fused kernel).
+    set_tuning "gcm_lanes" / "gcm_burst", reset afterwards."""
+    lanes, burst = request.param
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", lanes) == 0
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", split) == 0
     assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_burst", burst) == 0
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", bs) == 0
     try:
         yield lanes
     finally:
         drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_lanes", 0)
-        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0)
         drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_burst", 4096)
-        drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", 0)

@@ -7,11 +7,6 @@ import pytest
 
 import oracle as O
 
-# the measured-slower designs exist only in libespgpu_variants.so
-# (ESPGPU_VARIANTS=1, tests/conftest.py)
-VARIANTS = os.environ.get("ESPGPU_VARIANTS") == "1"
-variants_only = pytest.mark.skipif(not VARIANTS, reason="variants library only (ESPGPU_VARIANTS=1)")
-
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import VARIANTS, EtaSA, GcmSA, build_records, golden, oracle_decrypt, variants_only
+from helpers import EtaSA, GcmSA, build_records, golden, oracle_decrypt
 
 pytestmark = pytest.mark.gpu
 
@@ -270,25 +270,14 @@ def _mask_var(descs, size, hl, ml):
     return m
 
 
-@pytest.mark.parametrize("fused", [2, pytest.param(3, marks=variants_only), pytest.param(1, marks=variants_only),
-                                   pytest.param(0, marks=variants_only), pytest.param(4, marks=variants_only)])
 @pytest.mark.parametrize("esn", [False, True])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace, fused):
+def test_eta_variants_decrypt_vs_oracle(drv, esn, inplace):
     """AES-CBC / AES-CTR x HMAC-SHA1-96 / HMAC-SHA2 sessions mixed in one
     batch (planner path), AES-128/192/256, tag failures anywhere in the
     record: statuses and plaintext bit-exact vs the oracle, failed records
-    untouched in place.  fused (set_tuning eta_fused): 2 = the default
-    two-pass MODE 3 kernel out of place, 3 = verify and decrypt interleaved
-    (MODE 7), 1 = the one-pass fused MODE 0 kernels, 0 = the separate
-    verify + block-decrypt kernels, 4 = verify (MODE 6) beside the decrypt of
-    every valid record (MODE 8) on two streams."""
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
-    try:
-        _eta_variants_decrypt(drv, esn, inplace)
-    finally:
-        # the shared ctx goes back to the default kernels even when this fails
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+    untouched in place (MODE 2 in place, MODE 3 out of place)."""
+    _eta_variants_decrypt(drv, esn, inplace)
 
 
 def _full_icv_sas(rng):
@@ -366,14 +355,11 @@ def test_eta_full_hash_icv_vs_oracle(drv, inplace):
         drv.freesession(s)
 
 
-def test_eta_fused_knob_range(drv):
-    """eta_fused: 0..4, others EINVAL; the product library serves only the
-    default 2 (ENOTSUP for the measured-slower designs of the variants build)."""
-    for v in (-1, 5, 7):
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == 22
-    for v in (0, 1, 3, 4):
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", v) == (0 if VARIANTS else 95)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+def test_removed_design_knobs_are_unknown(drv):
+    """The measured-slower designs are not built: their old
+    set_tuning keys are unknown (ENOENT), not silently accepted."""
+    for k in (b"eta_fused", b"gcm_split", b"gcm_bs"):
+        assert drv.lib.espgpu_set_tuning(drv.ctx, k, 0) == 2
 
 
 def _eta_variants_decrypt(drv, esn, inplace):
@@ -441,19 +427,13 @@ def test_eta_variants_encrypt_vs_oracle(drv):
         drv.freesession(s)
 
 
-@pytest.mark.parametrize("fused", [2, pytest.param(3, marks=variants_only), pytest.param(4, marks=variants_only)])
-def test_eta_variants_trailer(drv, fused):
+def test_eta_variants_trailer(drv):
     """The fused esp_input_cb trailer word for CTR records (partial last
     block) and SHA2-256 sessions, out of place and in place; a record whose
-    ICV fails gets EBADMSG and trailer word 0 (eta_fused 3 and 4 decrypt it
-    out of place before its HMAC is known)."""
+    ICV fails gets EBADMSG and trailer word 0."""
     from espgpu.batch import decrypt_batch
     from espgpu.esp import trailer_word
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
-    try:
-        _eta_variants_trailer(drv, decrypt_batch, trailer_word)
-    finally:
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
+    _eta_variants_trailer(drv, decrypt_batch, trailer_word)
 
 
 def _eta_variants_trailer(drv, decrypt_batch, trailer_word):
@@ -691,18 +671,16 @@ def test_grouped_mode_mixed_run_fails_closed(drv):
         drv.freesession(s)
 
 
-@pytest.mark.parametrize("fused", [2, pytest.param(3, marks=variants_only)])
-def test_eta_mixed_sessions_in_one_wave_unit(drv, fused):
+def test_eta_mixed_sessions_in_one_wave_unit(drv):
     """Caller-grouped batch whose 64-record units mix ETA sessions (CBC +
-    HMAC-SHA1, CTR + HMAC-SHA2-256, CBC + HMAC-SHA2-384): eta_fused 3 takes
-    MODE 7's per-lane fallback (verify, then MODE 3's verified decrypt) for
-    such units, the wide-hash records go to their own launch; statuses and
-    verified plaintext vs the oracle, out of place, with tampered ICVs."""
+    HMAC-SHA1, CTR + HMAC-SHA2-256, CBC + HMAC-SHA2-384): one session at a
+    time through the verified decrypt, the wide-hash records in their own
+    launch; statuses and verified plaintext vs the oracle, out of place, with
+    tampered ICVs."""
     from espgpu.batch import decrypt_batch
-    rng = np.random.default_rng(1900 + fused)
+    rng = np.random.default_rng(1902)
     sas = [EtaSA(rng, 16), EtaSA(rng, 32, ctr=True, sha256=True), EtaSA(rng, 24, sha=384)]
     sids = _sessions(drv, sas)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", fused) == 0
     try:
         n = 640
         kinds = rng.integers(0, 3, n)
@@ -727,7 +705,6 @@ def test_eta_mixed_sessions_in_one_wave_unit(drv, fused):
         m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
         assert (out.cpu().numpy()[m_ok] == plain[m_ok]).all()
     finally:
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"eta_fused", 2) == 0
         for s in sids:
             drv.freesession(s)
 

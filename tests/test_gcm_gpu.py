@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import VARIANTS, GcmSA, build_records, golden, oracle_decrypt, variants_only
+from helpers import GcmSA, build_records, golden, oracle_decrypt
 
 pytestmark = pytest.mark.gpu
 
@@ -315,8 +315,7 @@ def test_invalid_records_einval(drv):
     drv.freesession(sids[0])
 
 
-@pytest.mark.parametrize("split", [0, pytest.param(1, marks=variants_only)], ids=["fused", "split"])
-def test_full_size_1m_x_1500_vs_oracle(drv, split):
+def test_full_size_1m_x_1500_vs_oracle(drv):
     """cfg1 at full size (1M x 1500-B packets, one AES-128-GCM SA), every
     record against the oracle: GPU encrypt gives the oracle's arena byte for
     byte; with 1% of the ICVs flipped, GPU decrypt gives the oracle's 1M
@@ -334,7 +333,6 @@ def test_full_size_1m_x_1500_vs_oracle(drv, split):
     d["len"] = rec
     d["salt"] = int.from_bytes(sas[0].salt, "little")
     nth = min(16, os.cpu_count() or 1)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", split) == 0
     ct = plain.copy()
     O.batch([sas[0].oracle], ct, d["off4"], d["len"], d["sa"], nthreads=nth, encrypt=True)
     d["sa"] = sids[0]
@@ -373,7 +371,6 @@ def test_full_size_1m_x_1500_vs_oracle(drv, split):
             assert np.array_equal(res[ok_mask], ref_out[ok_mask])
         del src, out, res
     drv.freesession(sids[0])
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0) == 0
 
 
 def test_freesession_waits_for_batch_on_user_stream(drv):
@@ -712,21 +709,6 @@ def test_grouped_batch_sizes_across_the_small_batch_path(drv, n):
     assert (arena.cpu().numpy() == ct).all()
     for s in sids:
         drv.freesession(s)
-
-
-def test_gcm_bs_knob_range(drv):
-    """set_tuning "gcm_bs" takes 0, 1, 2 (the bitsliced CTR pass) and refuses
-    anything else with EINVAL, leaving the setting unchanged; "gcm_split" 0
-    or 1.  The product library has neither design: ENOTSUP for anything but
-    0 (the variants library accepts them)."""
-    for v in (-1, 3, 9):
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == 22
-    for v in (2, 1):
-        assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", v) == (0 if VARIANTS else 95)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_bs", 0) == 0
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 2) == 22
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 1) == (0 if VARIANTS else 95)
-    assert drv.lib.espgpu_set_tuning(drv.ctx, b"gcm_split", 0) == 0
 
 
 @pytest.mark.parametrize("lanes,burst", [(0, 4096), (4, 4096), (8, 4096), (0, 1 << 30)],

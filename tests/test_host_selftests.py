@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_ghash_table_layout_selftest(tmp_path):
     """The 4-bit H^1..H^8 (global) GHASH tables, the 8-bit H^4 and H^8 tables
-    the GCM kernels expand from them in LDS (stage_h8 / ghash_expand8), and their stride-4 / stride-8 Horner + final
+    the GCM kernels expand from them in LDS (stage_h8_lds / ghash_expand8), and their stride-4 / stride-8 Horner + final
     H^(S-l) combination,
     against gf128_mul and a serial GHASH (tools/ghash_selftest.cpp)."""
     import re
@@ -29,32 +29,15 @@ def test_ghash_table_layout_selftest(tmp_path):
 
 
 def test_bitsliced_aes_selftest(tmp_path):
-    """The bitsliced AES of the gcm_bs ctr pass (aes_bs.h: the LUT3-packed
-    S-box circuit, key folding, affine constant in the round keys, 32x32
-    transposes), built for the CPU with its two gfx950 builtins emulated,
-    against host_crypto's table AES for AES-128/192/256 counter windows
-    (tools/aes_bs_selftest.cpp)."""
+    """The bitsliced AES the measurement probes run (tools/aes_bs.h: the
+    LUT3-packed S-box circuit, key folding, affine constant in the round keys,
+    32x32 transposes; tools/bsprobe.hip), built for the CPU with its two
+    gfx950 builtins emulated, against host_crypto's table AES for
+    AES-128/192/256 counter windows (tools/aes_bs_selftest.cpp)."""
     exe = tmp_path / "aes_bs_selftest"
     csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "tools"), "-I", csrc, "-o", str(exe),
                     os.path.join(ROOT, "tools", "aes_bs_selftest.cpp"),
-                    os.path.join(csrc, "host_crypto.cpp")], check=True, timeout=300)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-2000:]
-    assert r.stdout.startswith("OK")
-
-
-def test_quad_bitsliced_aes_selftest(tmp_path):
-    """The quad-bitsliced AES-128 counter step of the hybrid GCM switch
-    (esp_gcm.hip aes_ctr8_bsq, GCM_HYBRID: a record's 4 lanes hold one state
-    row each as bit planes, MixColumns across the quad), modelled lane by
-    lane on the CPU with aes_bs.h's S-box circuit and DevSA::dk's key form,
-    against host_crypto's table AES incl. counter runs that carry across
-    bytes (tools/bsq_selftest.cpp)."""
-    exe = tmp_path / "bsq_selftest"
-    csrc = os.path.join(ROOT, "f-stack_amd", "csrc")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-I", csrc, "-o", str(exe),
-                    os.path.join(ROOT, "tools", "bsq_selftest.cpp"),
                     os.path.join(csrc, "host_crypto.cpp")], check=True, timeout=300)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:]

@@ -1,5 +1,6 @@
-// Host self-test of the bitsliced AES (f-stack_amd/csrc/aes_bs.h) that the
-// bitsliced ctr pass (esp_gcm.hip gcm_bsctr_kernel, set_tuning "gcm_bs") runs:
+// Host self-test of the bitsliced AES (tools/aes_bs.h) that the measurement
+// probes run (tools/bsprobe.hip; round 3's bitsliced ctr pass, measured
+// slower and no longer built):
 // the header is built for the CPU with its two gfx950 builtins emulated
 // (v_bitop3_b32's truth table over a=0xf0, b=0xcc, c=0xaa; v_perm_b32's byte
 // select), and 32 counter blocks nonce || ctr are encrypted the kernel's way

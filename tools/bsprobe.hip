@@ -1,8 +1,8 @@
-// bsprobe.hip -- measurement only: bitsliced AES-128 (f-stack_amd/csrc/aes_bs.h)
+// bsprobe.hip -- measurement only: bitsliced AES-128 (tools/aes_bs.h)
 // throughput on gfx950, checked against a host AES first.  Each lane encrypts
 // 32 counter blocks nonce||ctr (ctr low 5 bits = the slice), all 10 rounds on
 // the VALU; the timing loop chains the state through `iters` encryptions.
-//   hipcc --offload-arch=gfx950 -O3 -I f-stack_amd/csrc -o tools/bsprobe tools/bsprobe.hip
+//   hipcc --offload-arch=gfx950 -O3 -I tools -I f-stack_amd/csrc -o tools/bsprobe tools/bsprobe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>

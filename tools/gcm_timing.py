@@ -27,10 +27,10 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--opts", type=int, nargs="*", default=[0],
                     help="measurement knobs (libespgpu built with make KNOBS=1): 1 no loads/stores, "
-                         "2 no GHASH, 4 no AES rounds 3+; bitsliced ctr pass (gcm_bs): 128 no rounds, "
-                         "256 no memory side, 512 no transposes")
+                         "2 no GHASH, 4 no AES rounds 3+, 8 no stores, 16 no loads, 32 no table staging, "
+                         "64 no final multiply")
     ap.add_argument("--grid", type=int, default=0)
-    ap.add_argument("--tuning", action="append", default=[], help="espgpu_set_tuning key=value (e.g. gcm_bs=1)")
+    ap.add_argument("--tuning", action="append", default=[], help="espgpu_set_tuning key=value (e.g. gcm_lanes=8)")
     args = ap.parse_args()
     import torch
     from espgpu.batch import decrypt_batch

@@ -1,7 +1,7 @@
 // Host self-test of the GHASH table layouts the GCM kernel uses
 // (host_crypto.cpp ghash_tables): the 4-bit H^1..H^8 tables (global,
 // gf_mul4_global) and the 8-bit H^4 / H^8 Horner tables the kernels expand
-// from them in LDS (stage_h8; ghash_expand8 is its host mirror, gf_mul8),
+// from them in LDS (stage_h8_lds; ghash_expand8 is its host mirror, gf_mul8),
 // each evaluated exactly the way esp_gcm.hip indexes it, against gf128_mul
 // (SP 800-38D Alg. 1).  Also the
 // stride-S Horner + final H^(S-l) combination, S = 4 and 8, against a serial

@@ -5,7 +5,7 @@
 // per CU by its 64 KiB LDS: one wave per SIMD at <= 128 VGPRs, T-table-shaped
 // rounds of 32 conflict-free ds_read_b32 each, as tools/ldsprobe.hip).  Times
 // each alone and both launched together; block-rounds per second of each.
-//   hipcc --offload-arch=gfx950 -O3 -I f-stack_amd/csrc -o tools/hybridprobe tools/hybridprobe.hip
+//   hipcc --offload-arch=gfx950 -O3 -I tools -I f-stack_amd/csrc -o tools/hybridprobe tools/hybridprobe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
