@@ -812,6 +812,114 @@ __device__ __forceinline__ void fill_pair(uint8_t *lds, uint32_t base, const uin
   }
 }
 
+// The verified decrypt of a wave unit (MODE 2 in place, MODE 3 to p.out):
+// run = this lane's record passed verification; (sa, off, plen, di, salt) its
+// session, offset, payload length, descriptor index and salt.  All of the
+// wave's blocks of one session as one flat list: records to decrypt (one
+// session at a time, so the round keys stay wave-uniform in SGPRs) are
+// concatenated; every lane takes one block per pass, last pass first.
+// Within a pass all lanes load their blocks (and C_{i-1}) before any lane
+// stores, and a pass only overwrites blocks no later (lower) pass reads:
+// in-place decryption is safe without holding records in registers.
+template <int MODE>
+__device__ __forceinline__ void verified_decrypt(const EtaParams &p, const uint8_t *lds, uint32_t slot, int lane,
+                                                 bool run, uint32_t sa, uint32_t off, uint32_t plen, uint32_t di,
+                                                 uint32_t salt) {
+  uint64_t todo = __ballot(run);
+  while (todo) {
+    const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
+    const bool mine = run && sa == sau;
+    todo &= ~__ballot(mine);
+    run = run && !mine;
+    const DevSA *s = p.sas + sau;
+    const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;      // wave-uniform
+    const bool null = s->calg == ESPGPU_CRYPTO_NULL_CBC;    // ESP-NULL: the identity
+    const uint32_t nb = mine ? (plen + 15) / 16 : 0;
+    uint32_t incl = nb;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const uint32_t start = incl - nb;
+    const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
+    const int nr = (int)s->nr;
+    // kEtaU blocks per lane per pass, 64 apart (each load instruction
+    // covers 64 consecutive blocks), decrypted together for ILP
+    constexpr int U = kEtaU;
+    for (int base = total - 64 * U; base > -64 * U; base -= 64 * U) {
+      int fk[U];
+      uint32_t ik[U], rok[U], rplk[U], rdik[U], rsk[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int f = base + lane + 64 * k;
+        // the record holding flat block f: the last lane whose start <= f
+        // (6-step shuffle search; by ballot and v_readlane it measured equal)
+        int j = 0;
+        uint32_t sj = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+          const uint32_t sc = __shfl(start, j + step);
+          if ((int)sc <= f) {
+            j += step;
+            sj = sc;
+          }
+        }
+        fk[k] = f;
+        ik[k] = (uint32_t)f - sj;
+        rok[k] = __shfl(off, j);
+        // (each __shfl is a ds_bpermute on the LDS pipe the AES lookups
+        // bound: only what the session kind uses, wave-uniform conditions)
+        rplk[k] = (ctr || null || p.trailer) ? __shfl(plen, j) : 0u;
+        rdik[k] = p.trailer ? __shfl(di, j) : 0u;
+        rsk[k] = ctr ? __shfl(salt, j) : 0u;
+      }
+      // all loads of the pass before any store (in place: see above)
+      uint4 v[U], pv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        v[k] = pv[k] = make_uint4(0, 0, 0, 0);
+        if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass loads
+          const uint8_t *rec = p.arena + rok[k];
+          if (null) {
+            v[k] = ld16(rec + 8 + 16 * ik[k]);                                     // P_i = C_i
+          } else if (ctr) {
+            pv[k] = ld16(rec + 16 + 16 * ik[k]);                                   // C_i
+            v[k] = make_uint4(rsk[k], *reinterpret_cast<const uint32_t *>(rec + 8),
+                              *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(ik[k] + 1));
+          } else {
+            v[k] = ld16(rec + 24 + 16 * ik[k]);                                    // C_i
+            pv[k] = ld16(rec + 8 + 16 * ik[k]);                // C_{i-1}, or the IV for i = 0
+          }
+        }
+      }
+      if (null) {
+      } else if (ctr) {
+        aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
+      } else if (!(eopts() & 0x40000)) {                       // knob: no decrypt-pass AES
+        aes_dec4(v, kp(s->dk), nr, lds, slot);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass stores
+          uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3: p.out (may be p.arena)
+          const uint32_t i = ik[k], rpl = rplk[k];
+          const int rem = (int)rpl - 16 * (int)i;
+          const uint4 pt = xor4(v[k], pv[k]);
+          if (null) {
+            if (MODE != 2 && p.out != p.arena) st_partial(dst + 8 + 16 * i, pt, rem);   // in place: as is
+          } else if (ctr) {
+            st_partial(dst + 16 + 16 * i, pt, rem);
+          } else {
+            st16(dst + 24 + 16 * i, pt);
+          }
+          if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdik[k]] = esp_trailer_word(last_word(pt, rem), rpl);
+        }
+      }
+    }
+  }
+}
+
 // MODE 1: encrypt, MAC pass over the ciphertext MODE 4 wrote (lane = record
 //         HMAC, ICV written);
 // MODE 2: decrypt in place, verify first: the verify pass (lane = record
@@ -1033,108 +1141,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_ke
     // decrypting a record's last block writes the others'
     if (have && p.trailer && !(valid && ok)) p.trailer[di] = 0;
 
-    // ---- verified decrypt: all of the wave's blocks of one session as one
-    // flat list ----
-    // Records to decrypt (one session at a time, so the round keys stay
-    // wave-uniform in SGPRs) are concatenated; every lane takes one block per
-    // pass, last pass first.  Within a pass all lanes load their blocks (and
-    // C_{i-1}) before any lane stores, and a pass only overwrites blocks no
-    // later (lower) pass reads: in-place decryption is safe without holding
-    // records in registers.
-    bool run = have && valid && ok;
-    uint64_t todo = __ballot(run);
-    while (todo) {
-      const uint32_t sau = __builtin_amdgcn_readfirstlane(__shfl(sa, __builtin_ctzll(todo)));
-      const bool mine = run && sa == sau;
-      todo &= ~__ballot(mine);
-      run = run && !mine;
-      const DevSA *s = p.sas + sau;
-      const bool ctr = s->calg == ESPGPU_CRYPTO_AES_ICM;      // wave-uniform
-      const bool null = s->calg == ESPGPU_CRYPTO_NULL_CBC;    // ESP-NULL: the identity
-      const uint32_t nb = mine ? (plen + 15) / 16 : 0;
-      uint32_t incl = nb;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-      }
-      const uint32_t start = incl - nb;
-      const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
-      const int nr = (int)s->nr;
-      // kEtaU blocks per lane per pass, 64 apart (each load instruction
-      // covers 64 consecutive blocks), decrypted together for ILP
-      constexpr int U = kEtaU;
-      for (int base = total - 64 * U; base > -64 * U; base -= 64 * U) {
-        int fk[U];
-        uint32_t ik[U], rok[U], rplk[U], rdik[U], rsk[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-          const int f = base + lane + 64 * k;
-          // the record holding flat block f: the last lane whose start <= f
-          // (6-step shuffle search; by ballot and v_readlane it measured equal)
-          int j = 0;
-          uint32_t sj = 0;
-#pragma unroll
-          for (int step = 32; step >= 1; step >>= 1) {
-            const uint32_t sc = __shfl(start, j + step);
-            if ((int)sc <= f) {
-              j += step;
-              sj = sc;
-            }
-          }
-          fk[k] = f;
-          ik[k] = (uint32_t)f - sj;
-          rok[k] = __shfl(off, j);
-          // (each __shfl is a ds_bpermute on the LDS pipe the AES lookups
-          // bound: only what the session kind uses, wave-uniform conditions)
-          rplk[k] = (ctr || null || p.trailer) ? __shfl(plen, j) : 0u;
-          rdik[k] = p.trailer ? __shfl(di, j) : 0u;
-          rsk[k] = ctr ? __shfl(salt, j) : 0u;
-        }
-        // all loads of the pass before any store (in place: see above)
-        uint4 v[U], pv[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-          v[k] = pv[k] = make_uint4(0, 0, 0, 0);
-          if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass loads
-            const uint8_t *rec = p.arena + rok[k];
-            if (null) {
-              v[k] = ld16(rec + 8 + 16 * ik[k]);                                     // P_i = C_i
-            } else if (ctr) {
-              pv[k] = ld16(rec + 16 + 16 * ik[k]);                                   // C_i
-              v[k] = make_uint4(rsk[k], *reinterpret_cast<const uint32_t *>(rec + 8),
-                                *reinterpret_cast<const uint32_t *>(rec + 12), bswap32(ik[k] + 1));
-            } else {
-              v[k] = ld16(rec + 24 + 16 * ik[k]);                                    // C_i
-              pv[k] = ld16(rec + 8 + 16 * ik[k]);                // C_{i-1}, or the IV for i = 0
-            }
-          }
-        }
-        if (null) {
-        } else if (ctr) {
-          aes_enc4(v, kp(s->rk), nr, lds + LDS_TE, slot);
-        } else if (!(eopts() & 0x40000)) {                       // knob: no decrypt-pass AES
-          aes_dec4(v, kp(s->dk), nr, lds, slot);
-        }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-          if (fk[k] >= 0 && !(eopts() & 0x80000)) {             // knob: no decrypt-pass stores
-            uint8_t *dst = (MODE == 2 ? p.arena : p.out) + rok[k];   // MODE 3: p.out (may be p.arena)
-            const uint32_t i = ik[k], rpl = rplk[k];
-            const int rem = (int)rpl - 16 * (int)i;
-            const uint4 pt = xor4(v[k], pv[k]);
-            if (null) {
-              if (MODE != 2 && p.out != p.arena) st_partial(dst + 8 + 16 * i, pt, rem);   // in place: as is
-            } else if (ctr) {
-              st_partial(dst + 16 + 16 * i, pt, rem);
-            } else {
-              st16(dst + 24 + 16 * i, pt);
-            }
-            if (p.trailer && i == (rpl + 15) / 16 - 1) p.trailer[rdik[k]] = esp_trailer_word(last_word(pt, rem), rpl);
-          }
-        }
-      }
-    }
+    verified_decrypt<MODE>(p, lds, slot, lane, have && valid && ok, sa, off, plen, di, salt);
   }
   // Every wave leaves the loop after drawing one ticket past the end, so once
   // all have retired no ticket is drawn again: reset for the next launch.

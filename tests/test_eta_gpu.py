@@ -355,10 +355,66 @@ def test_eta_full_hash_icv_vs_oracle(drv, inplace):
         drv.freesession(s)
 
 
+def test_eta_inplace_cbc_context_vs_oracle():
+    """In-place decrypt (MODE 2) of a CBC-only context at ~94 wave units:
+    SHA-1 and SHA2-256 sessions of every key size with ESN, beside SHA2-384
+    and cipher-only CBC sessions (the wide kernel's records), records of no
+    session and ragged CBC payloads (EINVAL), bit flips anywhere.  Statuses
+    and plaintext bit-exact vs the oracle, rejected records untouched, twice
+    (the retire resets the unit queue)."""
+    from espgpu.batch import decrypt_batch
+    from espgpu.opencrypto import GpuCryptoDriver
+    d0 = GpuCryptoDriver(max_sessions=64)
+    try:
+        rng = np.random.default_rng(1700)
+        sas = [EtaSA(rng, k, esn=e, sha=h) for k in (16, 24, 32) for e in (False, True) for h in (1, 256)] + \
+              [EtaSA(rng, 16, sha=384), EtaSA(rng, 32, noauth=True)]
+        sids = _sessions(d0, sas)
+        n = 6000                                  # ~94 units: several per wave
+        sa_idx = rng.integers(0, len(sas), n)
+        cts = rng.choice([16, 32, 48, 208, 1440, 1456, 8944], n)
+        eh = rng.integers(0, 2**32, n, dtype=np.uint32)
+        plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, esn_hi=eh)
+        bad = ct.copy()
+        flip = rng.random(n) < 0.07
+        for i in np.nonzero(flip)[0]:
+            o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+            bad[o + int(rng.integers(0, L))] ^= 0x20
+        ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+        d = descs.copy()
+        d["sa"] = [sids[s] for s in sa_idx]
+        orphan = rng.random(n) < 0.02
+        d["sa"][orphan] = 0xFFFF
+        ragged = ~orphan & (rng.random(n) < 0.02)
+        d["len"][ragged] -= 4
+        ref_st = ref_st.copy()
+        ref_st[orphan | ragged] = O.EINVAL
+        arena = _dev(bad)
+        st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            arena.copy_(_dev(bad))
+            st.fill_(0xEE)
+            decrypt_batch(d0, arena, _descs_dev(d), n, st, grouped=False)
+            torch.cuda.synchronize()
+            got = st.cpu().numpy()
+            assert (got == ref_st).all(), np.nonzero(got != ref_st)[0][:10]
+            hl, ml = _hl(sas, sa_idx)
+            ok = got == 0
+            m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
+            res = arena.cpu().numpy()
+            assert (res[m_ok] == ref_out[m_ok]).all()
+            m_bad = _mask_var(d[~ok], len(bad), np.zeros((~ok).sum()), np.zeros((~ok).sum()))
+            assert (res[m_bad] == bad[m_bad]).all()
+        for s in sids:
+            d0.freesession(s)
+    finally:
+        d0.close()
+
+
 def test_removed_design_knobs_are_unknown(drv):
     """The measured-slower designs are not built: their old
     set_tuning keys are unknown (ENOENT), not silently accepted."""
-    for k in (b"eta_fused", b"gcm_split", b"gcm_bs"):
+    for k in (b"eta_fused", b"gcm_split", b"gcm_bs", b"eta_ws", b"eta_lag"):
         assert drv.lib.espgpu_set_tuning(drv.ctx, k, 0) == 2
 
 
