@@ -368,18 +368,6 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *   "grid"      workgroups per launch (0 = 256, one per CU);
  *   "gcm_lanes" GCM lanes per record: 0 (default) 8 below 32768 records,
  *               else 4; 4 or 8 forces one kernel; others EINVAL;
- *   "gcm_split" GCM batches of >= 32768 records (or any size with gcm_lanes
- *               4): 1 = a CTR pass (16 lanes per record) then a GHASH / tag
- *               pass, 0 = the fused kernel;
- *   "gcm_bs"    GCM batches of >= 32768 records (or gcm_lanes 4): 1 = the
- *               bitsliced CTR pass (AES on the VALU, 32 counter blocks per
- *               lane) then the GHASH / tag pass; 2 = the same, out-of-place
- *               decrypt with the tag pass on a second stream; 0 (default) =
- *               by gcm_split; others EINVAL;
- *   "eta_fused" ETA decrypt kernels: 2 (default) verify pass + block-parallel
- *               decrypt (MODE 3) out of place, 1 one fused pass per record
- *               (MODE 0), 0 separate verify / decrypt kernels, 3 verify and
- *               decrypt interleaved per wave out of place (MODE 7); others EINVAL;
  *   "overflow_mb" host overflow for process() while every staging slot is
  *               in flight, in MiB (0, the default: ERESTART; 0..4095; only
  *               requests not yet moved into a slot count against it);
@@ -413,6 +401,8 @@ float espgpu_last_kernel_ms(espgpu_ctx *ctx);
  *   "gcm_opts" / "eta_opts" measurement knobs that skip work on purpose
  *               (results wrong): only in libespgpu_knobs.so, ENOTSUP in the
  *               product library unless 0.
+ * (The keys of designs measured slower and removed -- "gcm_split", "gcm_bs",
+ * "eta_fused", "eta_ws", "eta_lag" -- are unknown: ENOENT.)
  * Returns 0, EINVAL, ENOTSUP or ENOENT (unknown key). */
 #define ESPGPU_FAULT_LAUNCH 0x1
 #define ESPGPU_FAULT_QUERY  0x2
