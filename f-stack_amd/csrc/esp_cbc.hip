@@ -59,10 +59,6 @@ constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds (MODE 4)
 // that the common kernel carries no SHA-512 code (its registers then fit
 // without spilling): HMAC-SHA1 / SHA2-256 / none, or HMAC-SHA2-384 / 512 only
 constexpr int CK_NARROW = -2, CK_WIDEH = -3;
-#ifndef ETA_ENC_NB
-#define ETA_ENC_NB 1
-#define ETA_ENC_WAVES 8
-#endif
 constexpr int kEtaU = 4;               // blocks per lane per pass of the block-parallel decrypt
 constexpr int HS_SHA1 = 0, HS_SHA256 = 1;
 
@@ -938,7 +934,7 @@ __device__ __forceinline__ void verified_decrypt(const EtaParams &p, const uint8
 // or interleaved per wave; the in-place one pass with CBC rollback:
 // DESIGN.md §3.2, §5.1, §6.)
 template <int MODE, int WG, int CKS>
-__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? ETA_ENC_WAVES : 1) void eta_kernel(EtaParams p) {
+__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_kernel(EtaParams p) {
   static_assert(MODE >= 1 && MODE <= 4, "MAC pass, in-place / out-of-place decrypt, cipher pass");
   // (MODE 4 CBC: at least 8 waves per SIMD, <= 64 VGPRs, two workgroups per CU)
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
@@ -1080,7 +1076,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? ETA_ENC_WAVES : 1)
         const DevSA *s = p.sas + sau;
         const int nr = (int)s->nr;
         if (CKS == CK_CBC) {                      // (the whole wave: quad-coalesced 64-byte groups)
-          cbc_enc_quad<ETA_ENC_NB>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
+          cbc_enc_quad<1>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
           continue;
         }
         if (!mine) continue;
