@@ -10,7 +10,8 @@ configs 2-4), bit-exact against the oracle:
 
 Record counts are the full SA count and >= 64K records per configuration
 (per rank for cfg4); the oracle checks every record.  cfg1 at its full size
-(1M records) is checked record by record in test_gcm_gpu.py."""
+(1M records) is checked record by record in test_gcm_gpu.py, cfg2-4 in
+test_configs_full_gpu.py."""
 import numpy as np
 import pytest
 
@@ -167,9 +168,9 @@ def test_cfg4_rank_of_8_spi_shard(drv, rank):
 
 def test_planner_runs_of_one_session(drv):
     """Planner batch whose sessions hold hundreds of chunks each (4 GCM SAs x
-    ~200K records of two size classes): the GCM kernel draws runs of chunks
-    of one session at a time (GCM_GROUP) except in the queue's last 2 x grid
-    chunks; every record against the oracle, out of place and in place."""
+    ~200K records of two size classes, so a workgroup's consecutive tickets
+    are mostly of one session and it restages only on a change); every
+    record against the oracle, out of place and in place."""
     rng = np.random.default_rng(0xC5)
     nsa, n = 4, 800_000
     sas = [GcmSA(rng, 16) for _ in range(nsa)]
