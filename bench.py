@@ -501,6 +501,11 @@ def profile_traffic(config, inplace, kernel, kern_ms):
                       "avg_kernel_ms": pm.get("avg_kernel_ms")}
     if kernel in dom:
         out["traffic"] = pm.get("hbm_bytes_per_launch")
+        if pm.get("hbm_read_bytes_raw_per_launch") is not None:
+            # FETCH_SIZE x 1: the reads if every request were 64 B (quad-
+            # coalesced loads; traffic doubles them per the guide's rule, an
+            # upper bound for those kernels: profiles/r6_fetch_calibration.txt)
+            out["traffic_reads_raw"] = pm["hbm_read_bytes_raw_per_launch"]
         if pm.get("pipes"):
             # the compute resources of the same kernel: LDS-array and VALU-issue
             # busy shares and the floor each would set alone (tools/prof_summary.py)

@@ -6,7 +6,11 @@
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced read (16 B/lane loads), so it is doubled; WRITE_SIZE is exact for
-16-B/lane stores.
+16-B/lane stores.  FETCH_SIZE is TCC_EA0_RDREQ x 64 B for any request size,
+and quad-coalesced 64-byte groups (the ETA kernels' hash and CBC passes) make
+64-B requests, so for those the doubled figure is an upper bound and the raw
+one (hbm_read_bytes_raw_per_launch) a lower bound
+(profiles/r6_fetch_calibration.txt).
 
 `pipes` prices the kernel against its compute resources from the same counters
 (per launch; kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs):
@@ -102,6 +106,9 @@ def main():
         res["hbm_read_bytes_per_launch"] = rd
         res["hbm_write_bytes_per_launch"] = wr
         res["hbm_bytes_per_launch"] = rd + wr
+        # FETCH_SIZE x 1: the lower bound (64-B requests, the quad-coalesced
+        # reads of the ETA kernels: profiles/r6_fetch_calibration.txt)
+        res["hbm_read_bytes_raw_per_launch"] = c["FETCH_SIZE"] * 1024
     if "GRBM_GUI_ACTIVE" in c:
         res["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / ks[dominant]["avg_ns"]
         res["pipes"] = pipes(c, steady_ms or ks[dominant]["avg_ns"] / 1e6)
@@ -118,6 +125,9 @@ def main():
                        "avg_kernel_ms_all_calls": round(ks[dominant]["avg_ns"] / 1e6, 4),
                        "calls": ks[dominant]["calls"],
                        "hbm_bytes_per_launch": round(res["hbm_bytes_per_launch"]),
+                       "hbm_read_bytes_per_launch": round(res["hbm_read_bytes_per_launch"]),
+                       "hbm_read_bytes_raw_per_launch": round(res["hbm_read_bytes_raw_per_launch"]),
+                       "hbm_write_bytes_per_launch": round(res["hbm_write_bytes_per_launch"]),
                        "pipes": res.get("pipes")}, f, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
     print("dominant:", dominant, ks[dominant])
