@@ -844,6 +844,14 @@ __device__ __forceinline__ void verified_decrypt(const EtaParams &p, const uint8
     const uint32_t start = incl - nb;
     const int total = (int)__builtin_amdgcn_readfirstlane(__shfl(incl, 63));
     const int nr = (int)s->nr;
+    // Equal-length records in lanes 0..m-1 and none after (a planner unit
+    // of one MTU, as cfg3's): flat block f is block f - j*nbu of lane j =
+    // f / nbu, a multiply-shift (exact: f * nbu < 2^32) instead of the
+    // shuffle search's six ds_bpermutes on the LDS pipe
+    const uint64_t mm = __ballot(mine);
+    const uint32_t nbu = __builtin_amdgcn_readfirstlane(nb);   // lane 0's (mm has bit 0 if uniform)
+    const bool uni = (mm & (mm + 1)) == 0 && (mm & 1) && __all(!mine || nb == nbu) && nbu > 0;
+    const uint64_t inv = uni ? ((1ull << 32) + nbu - 1) / nbu : 0u;   // ceil(2^32 / nbu)
     // kEtaU blocks per lane per pass, 64 apart (each load instruction
     // covers 64 consecutive blocks), decrypted together for ILP
     constexpr int U = kEtaU;
@@ -857,12 +865,17 @@ __device__ __forceinline__ void verified_decrypt(const EtaParams &p, const uint8
         // (6-step shuffle search; by ballot and v_readlane it measured equal)
         int j = 0;
         uint32_t sj = 0;
+        if (uni) {                                    // (wave-uniform)
+          j = f < 0 ? 0 : (int)(((uint64_t)(uint32_t)f * inv) >> 32);   // = f / nbu
+          sj = (uint32_t)j * nbu;
+        } else {
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-          const uint32_t sc = __shfl(start, j + step);
-          if ((int)sc <= f) {
-            j += step;
-            sj = sc;
+          for (int step = 32; step >= 1; step >>= 1) {
+            const uint32_t sc = __shfl(start, j + step);
+            if ((int)sc <= f) {
+              j += step;
+              sj = sc;
+            }
           }
         }
         fk[k] = f;
