@@ -54,7 +54,9 @@ constexpr uint32_t LDS_SI = 65536;     // inverse S-box as dwords, [256][32], 32
 constexpr uint32_t LDS_TE = 98304;     // Te0/Te1 in the decrypt modes (CTR keystream), 64 KiB
 constexpr uint32_t lds_bytes(int mode) { return mode == 1 || mode == 4 ? 65536u : 163840u; }
 
-constexpr int CK_CBC = 0, CK_CTR = 1;   // cipher kinds (MODE 4)
+// cipher kinds (MODE 4): the CTR keystream, or the CBC chain with the
+// encrypt-then-MAC HMAC-SHA1 / SHA2-256 ICV in the same pass
+constexpr int CK_CTR = 1, CK_CBCMAC = 2;
 // MODE 1 / 2 / 3 session sets (the CKS template argument), split by hash so
 // that the common kernel carries no SHA-512 code (its registers then fit
 // without spilling): HMAC-SHA1 / SHA2-256 / none, or HMAC-SHA2-384 / 512 only
@@ -684,6 +686,132 @@ __device__ void cbc_enc_quad(bool act, uint8_t *rec, uint32_t nb0, kptr ek, int 
   }
 }
 
+// MODE 4 CK_CBCMAC: cbc_enc_quad's CBC chain with the HMAC of
+// encrypt-then-MAC in the same pass (xform_esp.c:673-961's output order:
+// encrypt, then the ICV over SPI|SN|IV|CT (|ESN hi), cryptosoft.c:874-888).
+// Each 64-byte ciphertext group the chain produces is hashed from the
+// lane's registers right away instead of being read back by a MAC pass:
+// SHA block g is message words 16g..16g+15, i.e. the 6 words before the
+// group (the 24-byte header for g = 0, else the previous group's last 6
+// ciphertext words) and the group's first 10 words.  The inner hash runs to
+// the wave's longest message (tail words as tail_word()), then the outer
+// hash and the ICV (mlen bytes after the ciphertext).  Every lane of the
+// wave calls it (act = this lane's record); ek / ipad / opad wave-uniform.
+template <int HS>
+__device__ void cbc_mac_quad(bool act, uint8_t *rec, uint32_t plen, kptr ek, int nr, const uint8_t *lds,
+                             uint32_t slot, bool esn, uint32_t esn_hi, kptr ipad, kptr opad, uint32_t mlen) {
+  constexpr int W = Hash<HS>::W;
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  const uint32_t nb = act ? plen / 16 : 0u;
+  const uint32_t l0w = 6u + plen / 4;                    // message words from the record
+  const uint32_t L = 4 * l0w + (esn ? 4u : 0u);          // message bytes
+  const uint32_t total = act ? (L + 9 + 63) / 64 : 0u;   // inner blocks incl. padding
+  const uint64_t bits = (uint64_t)(64 + L) * 8;          // the ipad block counts
+  const uint64_t rp = (uint64_t)(uintptr_t)rec;
+  const uint32_t rlo = (uint32_t)rp, rhi = (uint32_t)(rp >> 32);
+  auto pr = [&](auto I) {
+    constexpr int i = decltype(I)::value;
+    return (uint8_t *)(uintptr_t)(((uint64_t)qbcast<i>(rhi) << 32) | qbcast<i>(rlo));
+  };
+  auto pn = [&](auto I) { return qbcast<decltype(I)::value>(nb); };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  uint32_t nw = nb, gw = total;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    nw = max(nw, (uint32_t)__shfl_xor((int)nw, o));
+    gw = max(gw, (uint32_t)__shfl_xor((int)gw, o));
+  }
+  nw = __builtin_amdgcn_readfirstlane(nw);
+  gw = __builtin_amdgcn_readfirstlane(gw);
+  uint4 prev = act ? ld16(rec + 8) : make_uint4(0, 0, 0, 0);   // IV
+  // the 6 message words before the current group: SPI, SN, IV
+  uint32_t pw[6] = {act ? *reinterpret_cast<const uint32_t *>(rec) : 0u,
+                    act ? *reinterpret_cast<const uint32_t *>(rec + 4) : 0u, prev.x, prev.y, prev.z, prev.w};
+  uint32_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = (act && k < W) ? ipad[k] : 0u;
+  for (uint32_t g = 0; g < gw; ++g) {                 // wave-uniform trip count
+    const uint32_t b = 4 * g;
+    uint32_t X[4] = {0, 0, 0, 0}, Y[4] = {0, 0, 0, 0}, Z[4] = {0, 0, 0, 0}, V[4] = {0, 0, 0, 0};
+    if (b < nw) {                                     // (wave-uniform)
+      uint4 P[4];
+      auto ld = [&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint8_t *a = pr(I);                      // (DPP: every lane, outside the branch)
+        P[i] = b + q < pn(I) ? ld16(a + 24 + 16 * (b + q)) : make_uint4(0, 0, 0, 0);
+      };
+      ld(I0{});
+      ld(I1{});
+      ld(I2{});
+      ld(I3{});
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        X[i] = P[i].x;
+        Y[i] = P[i].y;
+        Z[i] = P[i].z;
+        V[i] = P[i].w;
+      }
+      quad_transpose4(X, qb0, qb1);
+      quad_transpose4(Y, qb0, qb1);
+      quad_transpose4(Z, qb0, qb1);
+      quad_transpose4(V, qb0, qb1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {                   // block b + k of this lane's record
+        if (b + k < nb) {
+          prev = aes_enc(xor4(make_uint4(X[k], Y[k], Z[k], V[k]), prev), ek, nr, lds, slot);
+          X[k] = prev.x;
+          Y[k] = prev.y;
+          Z[k] = prev.z;
+          V[k] = prev.w;
+        }
+      }
+    }
+    // SHA block g from the 6 words before the group and its first 10
+    const uint32_t c[16] = {X[0], Y[0], Z[0], V[0], X[1], Y[1], Z[1], V[1],
+                            X[2], Y[2], Z[2], V[2], X[3], Y[3], Z[3], V[3]};
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t m = 16 * g + (uint32_t)k;
+      uint32_t v = bswap32(k < 6 ? pw[k] : c[k - 6]);
+      if (m >= l0w) v = (esn && m == l0w) ? esn_hi : (4 * m == L ? 0x80000000u : 0u);
+      if (g + 1 == total && k == 14) v = (uint32_t)(bits >> 32);
+      if (g + 1 == total && k == 15) v = (uint32_t)bits;
+      w[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pw[k] = c[10 + k];
+    if (b < nw) {                                     // the ciphertext back, quad-coalesced
+      quad_transpose4(X, qb0, qb1);
+      quad_transpose4(Y, qb0, qb1);
+      quad_transpose4(Z, qb0, qb1);
+      quad_transpose4(V, qb0, qb1);
+      auto st = [&](auto I) {
+        constexpr int i = decltype(I)::value;
+        uint8_t *a = pr(I);                            // (DPP: every lane, outside the branch)
+        if (b + q < pn(I)) st16(a + 24 + 16 * (b + q), make_uint4(X[i], Y[i], Z[i], V[i]));
+      };
+      st(I0{});
+      st(I1{});
+      st(I2{});
+      st(I3{});
+    }
+    if (g < total) Hash<HS>::compress(h, w);
+  }
+  if (act) {
+    uint32_t w[16], o[8];
+    outer_block<HS>(h, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = k < W ? opad[k] : 0u;
+    Hash<HS>::compress(o, w);
+    for (uint32_t k = 0; k < mlen / 4; ++k) *reinterpret_cast<uint32_t *>(rec + 24 + plen + 4 * k) = bswap32(o[k]);
+  }
+}
+
 // ---- SHA-512 / SHA-384 compression (SHA512_Transform, freebsd/crypto/sha2/sha512c.c:196) ----
 // 64-bit words held as uint64_t; rotations as two v_alignbit on the halves.
 __constant__ uint64_t kK512[80] = ESPGPU_SHA512_K;
@@ -934,22 +1062,24 @@ __device__ __forceinline__ void verified_decrypt(const EtaParams &p, const uint8
 }
 
 // MODE 1: encrypt, MAC pass over the ciphertext MODE 4 wrote (lane = record
-//         HMAC, ICV written);
+//         HMAC, ICV written) for AES-CTR / ESP-NULL records and, at SHA2-384 /
+//         512, CBC ones;
 // MODE 2: decrypt in place, verify first: the verify pass (lane = record
 //         HMAC), then the block-parallel decrypt of the verified records;
 // MODE 3: decrypt out of place: the same two passes, plaintext to p.out;
-// MODE 4: encrypt, cipher pass (lane = record CBC chain / CTR keystream).
-// CKS: MODE 4 is built once per cipher (CK_CBC / CK_CTR); MODE 1 / 2 / 3 once
+// MODE 4: encrypt, cipher pass (lane = record CBC chain, with the HMAC-SHA1 /
+//         SHA2-256 ICV in the same pass; CTR keystream).
+// CKS: MODE 4 is built once per cipher (CK_CBCMAC / CK_CTR); MODE 1 / 2 / 3 once
 // per hash width (CK_NARROW: HMAC-SHA1 / SHA2-256 / no auth, no SHA-512 code,
 // so the registers fit without spilling; CK_WIDEH: HMAC-SHA2-384/512).
 // (Measured slower and not built: the one-pass out-of-place decrypt, the
 // verify and decrypt passes as separate kernels, side by side on two streams,
-// or interleaved per wave; the in-place one pass with CBC rollback:
-// DESIGN.md §3.2, §5.1, §6.)
+// or interleaved per wave; the in-place one pass with CBC rollback; wave-
+// specialised verify / decrypt roles and lagging waves; a CBC cipher pass at
+// 8 waves / SIMD followed by a MAC pass: DESIGN.md §3.2, §5.1, §5.2, §6.)
 template <int MODE, int WG, int CKS>
-__global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_kernel(EtaParams p) {
+__global__ __launch_bounds__(WG, 1) void eta_kernel(EtaParams p) {
   static_assert(MODE >= 1 && MODE <= 4, "MAC pass, in-place / out-of-place decrypt, cipher pass");
-  // (MODE 4 CBC: at least 8 waves per SIMD, <= 64 VGPRs, two workgroups per CU)
   __shared__ __attribute__((aligned(16))) uint8_t lds[lds_bytes(MODE)];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t slot = (uint32_t)(lane & 31) * 4;
@@ -1088,11 +1218,19 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_ke
         run = run && !mine;
         const DevSA *s = p.sas + sau;
         const int nr = (int)s->nr;
-        if (CKS == CK_CBC) {                      // (the whole wave: quad-coalesced 64-byte groups)
-          cbc_enc_quad<1>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
+        if (CKS == CK_CBCMAC) {                   // the chain and, for SHA-1 / SHA2-256, the ICV
+          const bool esn = (s->flags & ESPGPU_CSP_F_ESN) != 0;
+          if (s->aalg == ESPGPU_CRYPTO_SHA1_HMAC)
+            cbc_mac_quad<HS_SHA1>(mine, p.arena + off, plen, kp(s->rk), nr, lds, slot, esn, esnh, kp(s->ipad),
+                                  kp(s->opad), s->mlen);
+          else if (s->aalg == ESPGPU_CRYPTO_SHA2_256_HMAC)
+            cbc_mac_quad<HS_SHA256>(mine, p.arena + off, plen, kp(s->rk), nr, lds, slot, esn, esnh,
+                                    kp(s->ipad), kp(s->opad), s->mlen);
+          else                                    // no auth, or SHA2-384/512 (the wide MAC pass)
+            cbc_enc_quad<1>(mine, p.arena + off, plen / 16, kp(s->rk), nr, lds, slot);
           continue;
         }
-        if (!mine) continue;
+        if (CKS != CK_CTR || !mine) continue;
         uint8_t *rec = p.arena + off;
         const uint32_t iv0 = *reinterpret_cast<const uint32_t *>(rec + 8);
         const uint32_t iv1 = *reinterpret_cast<const uint32_t *>(rec + 12);
@@ -1109,6 +1247,9 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_ke
                          (int)(plen - 16 * (b + k)));
         }
       }
+      // the fused pass may be the only one for its records (no MAC pass when
+      // the ctx has no AES-CTR / ESP-NULL session)
+      if (CKS == CK_CBCMAC && have) p.status[di] = valid ? ESPGPU_OK : ESPGPU_EINVAL;
       continue;
     }
     if (MODE == 1) {
@@ -1117,7 +1258,7 @@ __global__ __launch_bounds__(WG, MODE == 4 && CKS == CK_CBC ? 8 : 1) void eta_ke
       // SHA-1 / SHA2-256 ICVs with hmac_quad's coalesced block loads (the whole
       // wave calls it), SHA2-384/512 with hmac_any
       int hq1 = 0;
-      if (have && valid) {
+      if (have && valid && p.sas[sa].calg != ESPGPU_CRYPTO_AES_CBC) {   // (CBC: the fused cipher pass's)
         const uint32_t aa = p.sas[sa].aalg;
         hq1 = aa == ESPGPU_CRYPTO_SHA1_HMAC ? 1 : aa == ESPGPU_CRYPTO_SHA2_256_HMAC ? 2 : 0;
       }
@@ -1190,12 +1331,18 @@ int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *strea
   };
   const int in_place = !encrypt && p.out == p.arena;
   if (encrypt) {
+    // Every CBC record's chain, and the ICV of the HMAC-SHA1 / SHA2-256
+    // ones, in one pass (CK_CBCMAC: the ciphertext is hashed from registers,
+    // not read back; cfg3 encrypt 2.56 -> 2.37 ms against a cipher pass then
+    // a MAC pass, profiles/r6_cfg3_fused_encrypt_ab.txt); the MAC pass then
+    // serves only AES-CTR / ESP-NULL records (none: not launched)
     if (kinds & 5)
-      hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBC>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
+      hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CBCMAC>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
     if (kinds & 10) hipLaunchKernelGGL((eta_kernel<4, 1024, CK_CTR>), dim3(clamp(2 * grid, 1024)), dim3(1024), 0, st, p);
     // MAC pass by hash width, as the decrypt: SHA-1 / SHA2-256 / no auth
     // without the SHA-512 code (1024 threads), SHA2-384/512 apart
-    hipLaunchKernelGGL((eta_kernel<1, 1024, CK_NARROW>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
+    if (kinds & 10)
+      hipLaunchKernelGGL((eta_kernel<1, 1024, CK_NARROW>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
     if (kinds & 16) hipLaunchKernelGGL((eta_kernel<1, 768, CK_WIDEH>), dim3(clamp(grid, 768)), dim3(768), 0, st, p);
   } else if (in_place) {
     hipLaunchKernelGGL((eta_kernel<2, 1024, CK_NARROW>), dim3(clamp(grid, 1024)), dim3(1024), 0, st, p);
