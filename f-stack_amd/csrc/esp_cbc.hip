@@ -70,8 +70,9 @@ typedef const __attribute__((address_space(4))) uint32_t *kptr;
 // (bench.py --tuning eta_opts=N with ESPGPU_LIB pointing at
 // libespgpu_knobs.so): 0x10000 skips the verify pass (every record decrypts),
 // 0x20000 the HMAC compressions (the loads stay), 0x40000 the decrypt pass's
-// AES, 0x80000 its loads and stores.  They break results on purpose, to split
-// the kernel's time.
+// AES, 0x80000 its loads and stores; in the fused CBC + HMAC encrypt pass
+// 0x100000 skips the stores, 0x200000 the loads, 0x400000 the compressions,
+// 0x800000 the AES.  They break results on purpose, to split the kernel's time.
 #ifdef ESPGPU_KNOBS
 __device__ uint32_t e_opts;
 __device__ __forceinline__ uint32_t eopts() {
@@ -493,6 +494,14 @@ __device__ __forceinline__ uint32_t qdpp(uint32_t x) {
 template <int I>
 __device__ __forceinline__ uint32_t qbcast(uint32_t x) { return qdpp<I * 0x55>(x); }   // quad_perm [I,I,I,I]
 
+// A record address rebuilt from its broadcast halves, as a global-memory
+// pointer: a plain integer-to-pointer cast is a generic (flat) address, and
+// flat loads and stores count in lgkmcnt too, beside the LDS table reads
+// (measured equal in time: profiles/r6_cfg3_encrypt_pipe_ab.txt).
+__device__ __forceinline__ uint8_t *gptr(uint64_t a) {
+  return (uint8_t *)(__attribute__((address_space(1))) uint8_t *)(uintptr_t)a;
+}
+
 // lane q of a quad: A[i] (i = 0..3) -> lane q holds, in A[k], lane k's A[q]
 __device__ __forceinline__ void quad_transpose4(uint32_t (&A)[4], bool qb0, bool qb1) {
 #pragma unroll
@@ -529,10 +538,10 @@ __device__ void hmac_quad(bool act, const uint8_t *rec, uint32_t L0, bool esn, u
   const uint64_t rp = (uint64_t)(uintptr_t)rec;
   const uint32_t rlo = (uint32_t)rp, rhi = (uint32_t)(rp >> 32);
   const uint8_t *pr[4] = {
-      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<0>(rhi) << 32) | qbcast<0>(rlo)),
-      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<1>(rhi) << 32) | qbcast<1>(rlo)),
-      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<2>(rhi) << 32) | qbcast<2>(rlo)),
-      (const uint8_t *)(uintptr_t)(((uint64_t)qbcast<3>(rhi) << 32) | qbcast<3>(rlo))};
+      gptr(((uint64_t)qbcast<0>(rhi) << 32) | qbcast<0>(rlo)),
+      gptr(((uint64_t)qbcast<1>(rhi) << 32) | qbcast<1>(rlo)),
+      gptr(((uint64_t)qbcast<2>(rhi) << 32) | qbcast<2>(rlo)),
+      gptr(((uint64_t)qbcast<3>(rhi) << 32) | qbcast<3>(rlo))};
   const uint32_t pn[4] = {qbcast<0>(nfull), qbcast<1>(nfull), qbcast<2>(nfull), qbcast<3>(nfull)};
   uint32_t tw = total;
 #pragma unroll
@@ -610,7 +619,7 @@ __device__ void cbc_enc_quad(bool act, uint8_t *rec, uint32_t nb0, kptr ek, int 
   const uint32_t rlo = (uint32_t)rp, rhi = (uint32_t)(rp >> 32);
   auto pr = [&](auto I) {
     constexpr int i = decltype(I)::value;
-    return (uint8_t *)(uintptr_t)(((uint64_t)qbcast<i>(rhi) << 32) | qbcast<i>(rlo));
+    return gptr(((uint64_t)qbcast<i>(rhi) << 32) | qbcast<i>(rlo));
   };
   auto pn = [&](auto I) { return qbcast<decltype(I)::value>(nb); };
   using I0 = std::integral_constant<int, 0>;
@@ -712,7 +721,7 @@ __device__ void cbc_mac_quad(bool act, uint8_t *rec, uint32_t plen, kptr ek, int
   const uint32_t rlo = (uint32_t)rp, rhi = (uint32_t)(rp >> 32);
   auto pr = [&](auto I) {
     constexpr int i = decltype(I)::value;
-    return (uint8_t *)(uintptr_t)(((uint64_t)qbcast<i>(rhi) << 32) | qbcast<i>(rlo));
+    return gptr(((uint64_t)qbcast<i>(rhi) << 32) | qbcast<i>(rlo));
   };
   auto pn = [&](auto I) { return qbcast<decltype(I)::value>(nb); };
   using I0 = std::integral_constant<int, 0>;
@@ -742,7 +751,7 @@ __device__ void cbc_mac_quad(bool act, uint8_t *rec, uint32_t plen, kptr ek, int
       auto ld = [&](auto I) {
         constexpr int i = decltype(I)::value;
         const uint8_t *a = pr(I);                      // (DPP: every lane, outside the branch)
-        P[i] = b + q < pn(I) ? ld16(a + 24 + 16 * (b + q)) : make_uint4(0, 0, 0, 0);
+        P[i] = b + q < pn(I) && !(eopts() & 0x200000) ? ld16(a + 24 + 16 * (b + q)) : make_uint4(0, 0, 0, 0);
       };
       ld(I0{});
       ld(I1{});
@@ -762,7 +771,8 @@ __device__ void cbc_mac_quad(bool act, uint8_t *rec, uint32_t plen, kptr ek, int
 #pragma unroll
       for (int k = 0; k < 4; ++k) {                   // block b + k of this lane's record
         if (b + k < nb) {
-          prev = aes_enc(xor4(make_uint4(X[k], Y[k], Z[k], V[k]), prev), ek, nr, lds, slot);
+          prev = (eopts() & 0x800000) ? xor4(make_uint4(X[k], Y[k], Z[k], V[k]), prev)
+                                      : aes_enc(xor4(make_uint4(X[k], Y[k], Z[k], V[k]), prev), ek, nr, lds, slot);
           X[k] = prev.x;
           Y[k] = prev.y;
           Z[k] = prev.z;
@@ -793,14 +803,14 @@ __device__ void cbc_mac_quad(bool act, uint8_t *rec, uint32_t plen, kptr ek, int
       auto st = [&](auto I) {
         constexpr int i = decltype(I)::value;
         uint8_t *a = pr(I);                            // (DPP: every lane, outside the branch)
-        if (b + q < pn(I)) st16(a + 24 + 16 * (b + q), make_uint4(X[i], Y[i], Z[i], V[i]));
+        if (b + q < pn(I) && !(eopts() & 0x100000)) st16(a + 24 + 16 * (b + q), make_uint4(X[i], Y[i], Z[i], V[i]));
       };
       st(I0{});
       st(I1{});
       st(I2{});
       st(I3{});
     }
-    if (g < total) Hash<HS>::compress(h, w);
+    if (g < total && !(eopts() & 0x400000)) Hash<HS>::compress(h, w);
   }
   if (act) {
     uint32_t w[16], o[8];

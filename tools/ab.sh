@@ -7,9 +7,9 @@
 #   bash tools/ab.sh [-r ROUNDS] [-c "cfg1 cfg4"] [-o OUT] [-x "bench args"] [-e] CAND...
 # (-e: also the encrypt leg; its kernel time is summarised as enc_ms)
 #
-# CAND = name=LIB[@key=val,key=val]: LIB a libespgpu.so (e.g. abl/<name>/libespgpu.so
+# CAND = name=LIB[@key=val,key=val][%bench-arg]: LIB a libespgpu.so (e.g. abl/<name>/libespgpu.so
 # from tools/variant.sh, or f-stack_amd/libespgpu.so), the optional @ list set_tuning
-# knobs.  Default bench args: in-place headline only (no side legs, no CPU).
+# knobs, the optional % one extra bench.py argument for this candidate.  Default bench args: in-place headline only (no side legs, no CPU).
 # Replaces round 4's one-off tools/r4_*.sh A/B scripts.
 set -euo pipefail
 ROUNDS=3; CFGS="cfg1"; OUT=gpurun_out/ab.jsonl; XARGS=""; ENC=--no-encrypt-leg
@@ -23,11 +23,13 @@ B=(python bench.py --steps 20 --warmup 10 --no-inplace-leg --no-cpu --no-e2e $EN
 for r in $(seq 1 "$ROUNDS"); do
   for cfg in $CFGS; do
     for cand in "$@"; do
-      name=${cand%%=*}; rest=${cand#*=}; lib=${rest%%@*}; knobs=""
+      name=${cand%%=*}; rest=${cand#*=}; carg=""
+      [[ $rest == *%* ]] && { carg=${rest#*%}; rest=${rest%%%*}; }
+      lib=${rest%%@*}; knobs=""
       [[ $rest == *@* ]] && knobs=${rest#*@}
       targs=()
       if [ -n "$knobs" ]; then IFS=, read -ra kv <<< "$knobs"; for k in "${kv[@]}"; do targs+=(--tuning "$k"); done; fi
-      line=$(ESPGPU_LIB=$lib timeout -k 10 180 "${B[@]}" --config "$cfg" "${targs[@]}" $XARGS 2>/dev/null | tail -1)
+      line=$(ESPGPU_LIB=$lib timeout -k 10 180 "${B[@]}" --config "$cfg" "${targs[@]}" $XARGS $carg 2>/dev/null | tail -1)
       python3 - "$name" "$cfg" "$r" "$knobs" "$line" <<'EOF' | tee -a "$OUT"
 import json, sys
 name, cfg, rnd, knobs, line = sys.argv[1:6]
