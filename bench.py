@@ -241,6 +241,8 @@ def main():
     ap.add_argument("--e2e-chunk", type=int, default=65536, help="records per pipelined step")
     ap.add_argument("--out-pad", type=int, default=0,
                     help="experiment: extra bytes per record in the out-of-place buffer (layout probes)")
+    ap.add_argument("--sizes", default="",
+                    help="experiment: comma list of packet sizes drawn uniformly instead of the config's")
     ap.add_argument("--sa-runs", action="store_true",
                     help="experiment: lay each SA's records out back to back (placement probe)")
     ap.add_argument("--dry-plan", action="store_true",
@@ -295,6 +297,10 @@ def main():
         cfg["workload"] += " [SA count overridden: %d]" % args.nsa
     rng = np.random.default_rng(0xE5B00001 + rank)
     spis, sa_of, sizes = plan_packets(cfg, rank, world, rng)
+    if args.sizes:
+        sizes = np.random.default_rng(0xE5B0000F + rank).choice(
+            np.array([int(x) for x in args.sizes.split(",")]), len(sizes))
+        cfg["workload"] += " [packet sizes overridden: %s]" % args.sizes
     if args.sa_runs:
         order = np.argsort(sa_of, kind="stable")
         sa_of, sizes = sa_of[order], sizes[order]
