@@ -1211,10 +1211,11 @@ __global__ __launch_bounds__(WG, 1) void eta_kernel(EtaParams p) {
     }
     if (MODE == 4) {
       // ---- encrypt, cipher pass (one kernel per cipher): lane = record.
-      // The CBC chain is serial (one AES state per lane), so it runs in a
-      // lean kernel (no hash code, few VGPRs, 2 workgroups x 16 waves per
-      // CU) where occupancy hides the round latency; CTR runs 4 blocks at a
-      // time ----
+      // CK_CBCMAC: the serial CBC chain (one AES state per lane) with the
+      // record's HMAC-SHA1 / SHA2-256 hashed from its registers (cbc_mac_quad,
+      // 113 VGPRs, 16 waves per CU; at 5 waves/SIMD it spills and runs 18 %
+      // slower); CK_CTR: the keystream 4 blocks at a time (the MAC pass
+      // follows) ----
       // One session at a time (a planner chunk has one): the session pointer
       // is wave-uniform, so the round keys come through the scalar cache into
       // SGPRs instead of a vector load per round on the CBC chain's critical
@@ -1328,8 +1329,9 @@ int set_eta_opts(uint32_t opts) {
 // Decrypt: 160 KiB of LDS, one workgroup per CU; the in-place SHA-1 /
 // SHA2-256 launch at 1024 threads (hmac_quad: 128 VGPRs, 4 waves/SIMD), the
 // others at 768 (3 waves/SIMD at up to 170 VGPRs: the unrolled hash schedules
-// need ~150).  Encrypt: the cipher passes at 1024 threads, up to two
-// workgroups per CU, then the MAC pass.
+// need ~150).  Encrypt: the fused CBC + HMAC pass and the CTR cipher pass at
+// 1024 threads (the CTR pass up to two workgroups per CU), then the MAC pass
+// for the CTR / ESP-NULL records only.
 int launch_eta(const EtaParams &p, int encrypt, int kinds, int grid, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (grid <= 0) grid = 256;
