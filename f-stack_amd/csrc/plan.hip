@@ -1,15 +1,16 @@
 // plan.hip — device-side batch planner: groups ESP records by (size class,
 // session) so that each 256-record chunk of the GCM kernel has ONE session
 // (its GHASH power tables and round keys are staged once in LDS) and records
-// of similar length share a wave.  Four small kernels, no host round trip:
-//   plan_count   per-workgroup LDS histogram of keys, flushed with one global
-//                atomic per non-empty key per workgroup
-//   plan_scan    one workgroup: exclusive scan of key counts -> record offsets
-//                and chunk offsets per key, the chunk count; zeroes the counts
-//   plan_emit    the chunk list, one chunk per thread (binary search of the
-//                per-key chunk offsets in LDS)
-//   plan_scatter per-workgroup LDS ranks + one global range reservation per
-//                non-empty key -> order[] (a permutation of descriptor ids)
+// of similar length share a wave.  Three small kernels, no host round trip:
+//   plan_count     per-workgroup LDS histogram of keys, flushed with one
+//                  global atomic per non-empty key per workgroup
+//   plan_scan_emit every workgroup: exclusive scan of the key counts ->
+//                  record and chunk offsets per key (in LDS), then its range
+//                  of the chunk list, one chunk per thread (binary search);
+//                  workgroup 0 writes the record cursors and chunk counts
+//   plan_scatter   per-workgroup LDS ranks + one global range reservation per
+//                  non-empty key -> order[] (a permutation of descriptor
+//                  ids); zeroes the counts for the next plan
 // Keys: [0, 4*nsas) = GCM records (class-major, largest class first),
 // 4*nsas = records with no valid session (chunked with sa = ~0 so the GCM
 // kernel marks them EINVAL), 4*nsas+1+s = records of ETA session s.  GCM and
@@ -72,40 +73,39 @@ __global__ __launch_bounds__(PWG) void plan_count(const espgpu_desc *desc, uint3
     if (hist[k]) atomicAdd(&gcnt[k], hist[k]);
 }
 
-// Single workgroup.  gcnt[nkeys] -> gcur[nkeys] (record cursor), and the
-// per-key first record and first chunk (groff / gcoff, nkeys + 1 entries)
-// that plan_emit turns into the chunk list.  Scan of the per-key record and
-// chunk counts: each thread sums a run of keys, Hillis-Steele over the 1024
-// partials.
-__global__ __launch_bounds__(PWG) void plan_scan(uint32_t *gcnt, uint32_t nsas, uint32_t *gcur,
-                                                 uint32_t *groff, uint32_t *gcoff, uint32_t *nchunks,
-                                                 uint32_t max_chunks) {
-  __shared__ uint32_t s_rec[PWG], s_chk[PWG];
-  __shared__ uint32_t s_cnt[kMaxLdsKeys];
+// The scan and the chunk list in one launch, by every workgroup of
+// ceil(max_chunks / PWG): each scans the per-key record and chunk counts
+// itself (~5K keys, 5 per thread: cheaper than a launch) into per-key first
+// record / first chunk offsets in LDS, then emits the chunks of its range
+// (chunk c belongs to the last key whose first chunk is <= c: binary search).
+// Workgroup 0 also writes the record cursors plan_scatter advances and the
+// chunk counts the crypto kernels read.  The counts are zeroed by
+// plan_scatter, after every workgroup here has read them.
+__global__ __launch_bounds__(PWG) void plan_scan_emit(const uint32_t *gcnt, uint32_t nsas, uint32_t *gcur,
+                                                      Chunk *chunks, uint32_t *nchunks, uint32_t max_chunks) {
+  __shared__ uint32_t s_rec[PWG / 64 + 1], s_chk[PWG / 64 + 1];
+  __shared__ uint32_t s_roff[kMaxLdsKeys + 1], s_coff[kMaxLdsKeys + 1];
   const uint32_t nkeys = num_keys(nsas);
   const uint32_t per = (nkeys + PWG - 1) / PWG;
   const uint32_t k0 = threadIdx.x * per, k1 = min(nkeys, k0 + per);
   const uint32_t eta0 = 4 * nsas + 1;                       // first ETA key
+  const bool lead = blockIdx.x == 0;
   static_assert(kChunkRecs == 256, "chunks_of: 256-record GCM chunks");
   // chunks of key k: 64-record ETA chunks, 256-record GCM / invalid ones
   // (shifts: a run-time divisor was a full integer division per key)
   auto chunks_of = [&](uint32_t k, uint32_t cnt) { return k >= eta0 ? (cnt + 63u) >> 6 : (cnt + 255u) >> 8; };
-  // The counts into LDS with coalesced, independent loads (a thread's run of
-  // keys read from global memory one dependent load after another was most
-  // of this kernel's time), then zeroed for the next plan: each thread clears
-  // what it loaded, so plan_count of the next batch starts from zero with no
-  // memset (the workspace's whole key capacity is zero between plans).
-  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) s_cnt[k] = gcnt[k];
+  // the counts into LDS with coalesced, independent loads (s_roff holds a
+  // key's count until its thread replaces it with the key's offset)
+  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) s_roff[k] = gcnt[k];
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) gcnt[k] = 0;
   uint32_t r = 0, c = 0;
   for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t cnt = s_cnt[k];
+    const uint32_t cnt = s_roff[k];
     r += cnt;
     c += chunks_of(k, cnt);
   }
   // inclusive scan of the 1024 partials: within each wave by shuffles, then
-  // over the 16 wave totals (3 barriers instead of Hillis-Steele's 20)
+  // over the 16 wave totals
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t ri = r, ci = c;
 #pragma unroll
@@ -136,47 +136,34 @@ __global__ __launch_bounds__(PWG) void plan_scan(uint32_t *gcnt, uint32_t nsas, 
   __syncthreads();
   uint32_t roff = s_rec[wave] + ri - r, coff = s_chk[wave] + ci - c;
   for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t cnt = s_cnt[k];
-    gcur[k] = roff;                       // record cursor (plan_scatter) = the key's first record
-    groff[k] = roff;
-    gcoff[k] = coff;
-    // the GCM kernel's share: the chunks before the first ETA key
-    if (k == eta0) nchunks[0] = min(coff, max_chunks);
+    const uint32_t cnt = s_roff[k];
+    s_roff[k] = roff;
+    s_coff[k] = coff;
+    if (lead) {
+      gcur[k] = roff;                      // record cursor (plan_scatter) = the key's first record
+      // the GCM kernel's share: the chunks before the first ETA key
+      if (k == eta0) nchunks[0] = min(coff, max_chunks);
+    }
     roff += cnt;
     coff += chunks_of(k, cnt);
   }
+  const uint32_t total = s_chk[PWG / 64];
   if (threadIdx.x == PWG - 1) {
-    const uint32_t total = s_chk[PWG / 64];
-    groff[nkeys] = s_rec[PWG / 64];
-    gcoff[nkeys] = total;
-    nchunks[1] = min(total, max_chunks);
-    if (eta0 >= nkeys) nchunks[0] = min(total, max_chunks);   // no ETA keys (no sessions)
-  }
-}
-
-// The chunk list, written by every thread of ceil(max_chunks / PWG)
-// workgroups (one workgroup emitting ~16K ETA chunks by binary search was
-// most of the planner's time): chunk c belongs to the last key whose first
-// chunk is <= c (binary search over the per-key offsets, staged in LDS).
-__global__ __launch_bounds__(PWG) void plan_emit(uint32_t nsas, const uint32_t *groff, const uint32_t *gcoff,
-                                                 Chunk *chunks, const uint32_t *nchunks) {
-  __shared__ uint32_t s_coff[kMaxLdsKeys + 1], s_roff[kMaxLdsKeys + 1];
-  const uint32_t lim = nchunks[1];
-  const uint32_t c0 = blockIdx.x * PWG;
-  if (c0 >= lim) return;                                  // workgroup-uniform
-  const uint32_t nkeys = num_keys(nsas);
-  const uint32_t eta0 = 4 * nsas + 1;
-  for (uint32_t k = threadIdx.x; k <= nkeys; k += PWG) {
-    s_coff[k] = gcoff[k];
-    s_roff[k] = groff[k];
+    s_roff[nkeys] = s_rec[PWG / 64];
+    s_coff[nkeys] = total;
+    if (lead) {
+      nchunks[1] = min(total, max_chunks);
+      if (eta0 >= nkeys) nchunks[0] = min(total, max_chunks);   // no ETA keys (no sessions)
+    }
   }
   __syncthreads();
-  const uint32_t ci = c0 + threadIdx.x;
-  if (ci >= lim) return;
-  uint32_t lo = 0, hi = nkeys;                            // last key with s_coff <= ci
+  const uint32_t lim = min(total, max_chunks);
+  const uint32_t cc = blockIdx.x * PWG + threadIdx.x;
+  if (cc >= lim) return;
+  uint32_t lo = 0, hi = nkeys;                            // last key with s_coff <= cc
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (s_coff[mid] <= ci) lo = mid;
+    if (s_coff[mid] <= cc) lo = mid;
     else hi = mid;
   }
   const uint32_t k = lo, cnt = s_roff[k + 1] - s_roff[k], rpc = k >= eta0 ? 64u : (uint32_t)kChunkRecs;
@@ -186,16 +173,19 @@ __global__ __launch_bounds__(PWG) void plan_emit(uint32_t nsas, const uint32_t *
   // 256 + 14): a workgroup's pass time grows with its busy waves, so a
   // near-empty remainder chunk costs almost a full pass (cfg2: 1K sessions
   // x 4 size classes leave ~256 +- 16 records per key)
-  const uint32_t nc = (cnt + rpc - 1) / rpc, jj = ci - s_coff[k];
+  const uint32_t nc = (cnt + rpc - 1) / rpc, jj = cc - s_coff[k];
   const uint32_t a = (uint32_t)((uint64_t)cnt * jj / nc), b = (uint32_t)((uint64_t)cnt * (jj + 1) / nc);
-  chunks[ci] = Chunk{sa, s_roff[k] + a, b - a, cls};
+  chunks[cc] = Chunk{sa, s_roff[k] + a, b - a, cls};
 }
 
 __global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uint32_t n,
                                                     const DevSA *sas, uint32_t nsas,
-                                                    uint32_t *gcur, uint32_t *order) {
+                                                    uint32_t *gcur, uint32_t *order, uint32_t *gcnt) {
   __shared__ uint32_t hist[kMaxLdsKeys], lbase[kMaxLdsKeys];
   const uint32_t nkeys = num_keys(nsas);
+  // the counts plan_scan_emit has read, zeroed for the next plan (so the
+  // workspace's whole key capacity is zero between plans: no memset)
+  for (uint32_t k = blockIdx.x * PWG + threadIdx.x; k < nkeys; k += gridDim.x * PWG) gcnt[k] = 0;
   for (uint32_t k = threadIdx.x; k < nkeys; k += PWG) hist[k] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * TILE;
@@ -222,7 +212,8 @@ __global__ __launch_bounds__(PWG) void plan_scatter(const espgpu_desc *desc, uin
 
 }  // namespace
 
-// gcnt, gcur: one word per key; groff, gcoff: one more (the totals)
+// gcnt, gcur: one word per key; groff, gcoff (unused since the scan and the
+// chunk list share a launch; the layout is kept): one more
 size_t plan_workspace_words(uint32_t nsas) { return 4 * (size_t)num_keys(nsas) + 2; }
 uint32_t plan_max_chunks(uint32_t n, uint32_t nsas) { return n / 64 + num_keys(nsas) + 8; }
 
@@ -237,14 +228,13 @@ int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_
   // keys: the key count grows with the session table, and cursor words left
   // where a later batch's counts go would be counted
   const uint32_t capk = num_keys(cap_sas);
-  uint32_t *gcnt = d_work, *gcur = d_work + capk, *groff = gcur + capk, *gcoff = groff + capk + 1;
+  uint32_t *gcnt = d_work, *gcur = d_work + capk;
   const uint32_t grid = (n + TILE - 1) / TILE;
   if (grid) hipLaunchKernelGGL(plan_count, dim3(grid), dim3(PWG), 0, st, d_desc, n, sas, nsas, gcnt);
-  hipLaunchKernelGGL(plan_scan, dim3(1), dim3(PWG), 0, st, gcnt, nsas, gcur, groff, gcoff, d_nchunks, max_chunks);
-  hipLaunchKernelGGL(plan_emit, dim3((max_chunks + PWG - 1) / PWG), dim3(PWG), 0, st, nsas, groff, gcoff, d_chunks,
-                     d_nchunks);
+  hipLaunchKernelGGL(plan_scan_emit, dim3((max_chunks + PWG - 1) / PWG), dim3(PWG), 0, st, gcnt, nsas, gcur,
+                     d_chunks, d_nchunks, max_chunks);
   if (grid) hipLaunchKernelGGL(plan_scatter, dim3(grid), dim3(PWG), 0, st, d_desc, n, sas, nsas, gcur,
-                               d_order);
+                               d_order, gcnt);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
