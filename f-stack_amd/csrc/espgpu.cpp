@@ -99,6 +99,9 @@ struct Overflow {
     FifoArena<uint8_t> b;
     FifoArena<espgpu_seg> sg;
     if ((ne && !e) || !b.init(cap_bytes) || !sg.init(ne * 4)) return false;
+    // the entry ring's pages committed now too, as the arenas' (fifo_arena.h)
+    for (size_t o = 0; o < ne * sizeof(OvfEntry); o += 4096)
+      reinterpret_cast<volatile uint8_t *>(e.get())[o] = 0;
     ent.swap(e);
     ecap = ne;
     bytes.swap(b);

@@ -7,6 +7,7 @@
 
 #include <memory>
 #include <new>
+#include <type_traits>
 
 namespace espgpu {
 
@@ -26,6 +27,12 @@ struct FifoArena {
     if (n) {
       p = new (std::nothrow) T[n];
       if (!p) return false;
+      if constexpr (std::is_trivially_default_constructible<T>::value) {
+        // commit the pages now, one write each: process() then takes no
+        // first-touch page fault inside its non-blocking bound
+        volatile uint8_t *b = reinterpret_cast<volatile uint8_t *>(p);
+        for (size_t o = 0; o < n * sizeof(T); o += 4096) b[o] = 0;
+      }
     }
     buf.reset(p);
     cap = n;
