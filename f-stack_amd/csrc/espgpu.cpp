@@ -599,6 +599,19 @@ void drop_slot(espgpu_ctx *c, Slot &s) {
   s.state = SLOT_FREE;
 }
 
+// A batch about to be released as failed: work of it still queued may write
+// the requests' host buffers (zero-copy results, the results' xfer kernel), so
+// wait for its completion event, at most deadline_ms, first (as fail_launch
+// does for a launch that failed part way).  A query error ends the wait: the
+// device runs nothing of it any more.
+void slot_settle(espgpu_ctx *c, Slot &s) {
+  const uint64_t t0 = now_ns();
+  while (hipEventQuery(s.done) == hipErrorNotReady) {
+    if (now_ns() - t0 > (uint64_t)c->deadline_ms * 1000000ull) return;
+    sched_yield();
+  }
+}
+
 // Mark the ctx failed (once) and release what was never handed to the
 // device: the filling slot and the host overflow.  In-flight batches are
 // retired by poll / drain (slot_check).  Returns ESPGPU_EIO.
@@ -626,7 +639,8 @@ int ctx_fail(espgpu_ctx *c, const char *why) {
 // (its completion query returned an error, it outlived deadline_ms, or the ctx
 // failed and the batch can no longer finish).  A doorbell job of a failed ctx
 // is released only once the kernel has exited (a workgroup inside one of its
-// chunks still writes results into host memory) or after the deadline.
+// chunks still writes results into host memory) or after the deadline; any
+// other failed batch once its queued work has drained (slot_settle).
 int slot_check(espgpu_ctx *c, Slot &s, uint64_t now) {
   const bool late = now > s.t_launch && now - s.t_launch > (uint64_t)c->deadline_ms * 1000000ull;
   if (s.door_job >= 0) {
@@ -646,10 +660,12 @@ int slot_check(espgpu_ctx *c, Slot &s, uint64_t now) {
       c->err = hipGetErrorString(q);
       ctx_fail(c, "batch completion query failed");
     }
+    slot_settle(c, s);
     return -1;
   }
   if (!late) return 0;
   if (!c->failed) ctx_fail(c, "batch outstanding past deadline_ms");
+  slot_settle(c, s);
   return -1;
 }
 
