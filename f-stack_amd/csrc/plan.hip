@@ -223,7 +223,7 @@ int launch_plan(const espgpu_desc *d_desc, uint32_t n, const DevSA *sas, uint32_
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const uint32_t nkeys = num_keys(nsas);
   if (nkeys > kMaxLdsKeys || nsas > cap_sas) return -1;   // caller must pre-group (ESPGPU_BATCH_GROUPED)
-  // gcnt is zero on entry (plan_scan re-zeroes it) over the workspace's whole
+  // gcnt is zero on entry (plan_scatter re-zeroes it) over the workspace's whole
   // key capacity; the cursors sit after that capacity, not after this batch's
   // keys: the key count grows with the session table, and cursor words left
   // where a later batch's counts go would be counted
