@@ -744,7 +744,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
   if (!(flags & ESPGPU_BATCH_GROUPED)) {
     int e = ensure_plan(c, n);
     if (e) return e;
-    // the key counts start at zero: plan_scan zeroes them after reading, so
+    // the key counts start at zero: plan_scatter zeroes them after use, so
     // only a fresh workspace (or one a failed launch left behind) needs it
     if (c->plan_dirty) {
       HIPCHK(c, hipMemsetAsync(c->d_work, 0, plan_workspace_words(c->cfg.max_sessions) * 4, st));
@@ -753,7 +753,7 @@ int run_batch(espgpu_ctx *c, uint8_t *d_arena, const espgpu_desc *d_desc, uint32
     if (launch_plan(d_desc, n, c->d_sas, nsas, c->cfg.max_sessions, c->d_work, c->d_order, c->d_chunks, c->d_nchunks,
                     c->max_chunks, st)) {
       c->plan_dirty = true;
-      return fail(c, ESPGPU_ENOTSUP, "planner: too many sessions for device grouping (%u); pre-group and pass ESPGPU_BATCH_GROUPED", nsas);
+      return fail(c, ESPGPU_EIO, "planner launch failed (%u sessions)", nsas);
     }
     p.order = c->d_order;
     p.chunks = c->d_chunks;

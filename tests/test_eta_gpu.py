@@ -810,3 +810,55 @@ def test_planner_as_the_session_table_grows():
             assert (out.cpu().numpy()[m_ok] == ref_out[m_ok]).all()
     finally:
         d.close()
+
+
+def test_planner_past_the_lds_key_arrays():
+    """A session table with more planner keys (5 x sessions + 1) than the
+    LDS arrays hold (16384: 3276 sessions) takes the global-memory plan
+    (plan.hip plan_*_g).  A batch at 3276 sessions (the LDS plan's last size)
+    and one at 3400, GCM and ETA sessions mixed, records in random session
+    order with 10 % tampered ICVs, out of place and in place: statuses and
+    plaintext vs the oracle, the tampered records in place restored."""
+    from espgpu.batch import decrypt_batch
+    from espgpu.opencrypto import GpuCryptoDriver
+    d = GpuCryptoDriver(max_sessions=4096)
+    try:
+        rng = np.random.default_rng(3276)
+        sas, sids = [], []
+        for total in (3276, 3400):
+            new = [GcmSA(rng, 16) if rng.random() < 0.8 else EtaSA(rng, 16, sha256=bool(rng.random() < 0.5))
+                   for _ in range(total - len(sas))]
+            sids += _sessions(d, new)
+            sas += new
+            n = 12000
+            sa_idx = rng.integers(0, len(sas), n)
+            cts = np.where([isinstance(sas[i], GcmSA) for i in sa_idx], rng.integers(1, 90, n) * 16 - 4,
+                           rng.integers(1, 90, n) * 16)
+            eh = np.zeros(n, dtype=np.uint32)
+            plain, ct, descs, eh = build_records(rng, sas, sa_idx, cts, esn_hi=eh)
+            bad = ct.copy()
+            for i in np.nonzero(rng.random(n) < 0.1)[0]:
+                o, L = int(descs["off4"][i]) * 4, int(descs["len"][i])
+                bad[o + L - 1] ^= 0x01                          # inside the ICV
+            ref_out, ref_st = oracle_decrypt(sas, bad, descs, eh)
+            assert (ref_st != 0).any() and (ref_st == 0).any()
+            dd = descs.copy()
+            dd["sa"] = [sids[s] for s in sa_idx]
+            hl, ml = _hl(sas, sa_idx)
+            for inplace in (False, True):
+                arena = _dev(bad)
+                out = arena if inplace else torch.zeros_like(arena)
+                st = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+                decrypt_batch(d, arena, _descs_dev(dd), n, st, out=None if inplace else out, grouped=False)
+                torch.cuda.synchronize()
+                got = st.cpu().numpy()
+                assert (got == ref_st).all(), (len(sas), inplace, np.nonzero(got != ref_st)[0][:10])
+                ok = got == 0
+                m_ok = _mask_var(descs[ok], len(bad), hl[ok], ml[ok])
+                res = out.cpu().numpy()
+                assert (res[m_ok] == ref_out[m_ok]).all(), (len(sas), inplace)
+                if inplace:
+                    m_bad = _mask_var(descs[~ok], len(bad), hl[~ok], ml[~ok])
+                    assert (res[m_bad] == bad[m_bad]).all(), len(sas)      # failed records untouched
+    finally:
+        d.close()
