@@ -1100,6 +1100,13 @@ int espgpu_newsession(espgpu_ctx *c, const espgpu_session_params *csp, int32_t *
   return 0;
 }
 
+int espgpu_session_room(espgpu_ctx *c) {
+  if (!c) return ESPGPU_EINVAL;
+  size_t room = c->cfg.max_sessions - c->sessions.size();
+  for (const Session &s : c->sessions) room += s.used ? 0 : 1;
+  return (int)std::min<size_t>(room, INT32_MAX);
+}
+
 void espgpu_freesession(espgpu_ctx *c, int32_t sid) {
   if (!c || sid < 0 || (size_t)sid >= c->sessions.size() || !c->sessions[sid].used) return;
   if (!c->failed) {

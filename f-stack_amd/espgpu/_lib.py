@@ -131,6 +131,8 @@ def lib():
         L.espgpu_newsession.argtypes = [vp, C.POINTER(SessionParams), C.POINTER(C.c_int32)]
         L.espgpu_freesession.argtypes = [vp, C.c_int32]
         L.espgpu_freesession.restype = None
+        L.espgpu_session_room.argtypes = [vp]
+        L.espgpu_session_room.restype = C.c_int
         L.espgpu_process.argtypes = [vp, C.POINTER(Req), C.c_int]
         L.espgpu_flush.argtypes = [vp]
         L.espgpu_poll.argtypes = [vp, C.POINTER(Completion), C.c_int]

@@ -167,6 +167,10 @@ class GpuCryptoDriver:
         """0, or EIO once the GPU failed (espgpu_health)"""
         return self.lib.espgpu_health(self.ctx)
 
+    def session_room(self):
+        """Free SA-table slots (espgpu_session_room): at 0 newsession is ENOMEM"""
+        return self.lib.espgpu_session_room(self.ctx)
+
     def flush(self):
         rc = self.lib.espgpu_flush(self.ctx)
         # EIO: the GPU failed; the held requests come back through poll()

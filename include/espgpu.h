@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define ESPGPU_ABI_VERSION 5
+#define ESPGPU_ABI_VERSION 6
 
 /* ---- constants, numerically identical to freebsd/opencrypto/cryptodev.h ---- */
 #define ESPGPU_CSP_MODE_CIPHER      2        /* cryptodev.h:362: ESP without auth */
@@ -203,6 +203,11 @@ int  espgpu_newsession(espgpu_ctx *ctx, const struct espgpu_session_params *csp,
                        int32_t *session_out);
 /* CRYPTODEV_FREESESSION (cryptodev_if.m:113-116) */
 void espgpu_freesession(espgpu_ctx *ctx, int32_t session);
+/* Free SA-table slots (ABI 6; >= 0, or ESPGPU_EINVAL without a context):
+ * at 0 espgpu_newsession answers ESPGPU_ENOMEM.  The F-Stack shim's probe
+ * declines then, so crypto_newsession selects cryptosoft instead of failing
+ * the SA in CRYPTODEV_NEWSESSION (crypto.c:954-958). */
+int  espgpu_session_room(espgpu_ctx *ctx);
 /* CRYPTODEV_PROCESS (cryptodev_if.m:143-147): never blocks.  On a failed
  * context (espgpu_health) it answers ESPGPU_EIO at once: never ERESTART or
  * EAGAIN, which would hand the request back to this dead engine.  Stages the

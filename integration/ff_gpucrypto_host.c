@@ -133,9 +133,17 @@ int ff_gpucrypto_host_failed(void)
  * Host-only, valid before ff_gpucrypto_host_init. */
 int ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
 {
+	int r;
+
 	if (ff_gpucrypto_host_failed())
 		return ESPGPU_ENXIO;
-	return espgpu_probesession(csp);
+	r = espgpu_probesession(csp);
+	/* a full SA table declines here, so that crypto_newsession selects
+	 * cryptosoft rather than failing the SA in CRYPTODEV_NEWSESSION
+	 * (crypto.c:954-958) */
+	if (r == ESPGPU_PROBE_HARDWARE && g_ctx && espgpu_session_room(g_ctx) == 0)
+		return ESPGPU_ENOMEM;
+	return r;
 }
 
 int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid)

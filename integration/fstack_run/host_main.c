@@ -18,6 +18,7 @@
  *   4. every request crypto_dispatch'ed on both (mbuf chains or contiguous
  *      buffers), main_loop's ff_gpucrypto_poll() until each callback has run
  *      (crypto_done inline: no crypto_ret thread runs in F-Stack);
+ *   4b. without --fail, a full SA table: the next session goes to cryptosoft
  *   5. with --fail, the GPU-failure path: the engine
  *      fails (GPU build: set_tuning "fault" 1, the next launch fails; CPU
  *      build: the stand-in fails with the requests staged), every request is
@@ -181,6 +182,41 @@ main(int argc, char **argv)
 		if (rsw[i] == NULL)
 			die("request");
 		disp[2 * i + 1] = ffst_dispatch(rsw[i]);
+	}
+
+	/* 4b. a full SA table: new sessions on the parameters of a session the
+	 * driver holds, until one lands on cryptosoft -- the probe declines on a
+	 * full table, where CRYPTODEV_NEWSESSION failing would fail the SA
+	 * (crypto.c:954-958) -- then, with one GPU session freed, the next lands
+	 * on the GPU again */
+	if (!fail) {
+		enum { MAXS = 8192 };
+		void **xs = calloc(MAXS, sizeof(void *));
+		int nx = 0, ngpu = 0, err = 0, hid = -1, g = -1;
+		for (uint32_t i = 0; i < nses && g < 0; i++)
+			if (sinfo[4 * i + 1] == gpu_hid)
+				g = (int)i;
+		if (g < 0)
+			die("SA-table fill: no session on gpucrypto");
+		while (nx < MAXS) {
+			xs[nx] = ffst_newsession(ss[g].p, ss[g].ckey, ss[g].akey, CAP_HW | CAP_SW, &err, &hid);
+			if (xs[nx] == NULL)
+				die("SA-table fill: crypto_newsession failed");
+			nx++;
+			if (hid != gpu_hid)
+				break;
+			ngpu++;
+		}
+		if (hid != sw_hid || ngpu == 0)
+			die("SA-table fill: the full table did not hand the session to cryptosoft");
+		ffst_freesession(xs[0]);
+		xs[0] = ffst_newsession(ss[g].p, ss[g].ckey, ss[g].akey, CAP_HW | CAP_SW, &err, &hid);
+		if (xs[0] == NULL || hid != gpu_hid)
+			die("SA-table fill: a freed slot was not reused");
+		for (int i = 0; i < nx; i++)
+			ffst_freesession(xs[i]);
+		free(xs);
+		printf("SA table full after %d more sessions on gpucrypto: the next went to cryptosoft\n", ngpu);
 	}
 
 	/* 5. the GPU-failure phase: f1 = the requests the engine holds when it

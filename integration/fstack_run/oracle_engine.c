@@ -50,9 +50,18 @@ void oracle_engine_fail(void) { g_failed = 1; }
 int
 ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
 {
+	int r;
+
 	if (g_failed)
 		return (ESPGPU_ENXIO);
-	return (espgpu_probesession(csp));
+	r = espgpu_probesession(csp);
+	if (r != ESPGPU_PROBE_HARDWARE)
+		return (r);
+	/* a full SA table declines (ff_gpucrypto_host.c: espgpu_session_room) */
+	for (int i = 0; i < OE_MAX_SES; i++)
+		if (!g_ses[i].used)
+			return (r);
+	return (ESPGPU_ENOMEM);
 }
 
 int

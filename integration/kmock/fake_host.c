@@ -19,7 +19,7 @@ void ff_gpucrypto_done(void *opaque, int abi_etype);
 void ff_gpucrypto_unblock(void);
 
 static struct { void *opaque; int etype; } staged[FAKE_CAP];
-static int nstaged, next_sid, failed;
+static int nstaged, next_sid, nfreed, failed;
 int fake_freed_sid = -1, fake_last_nsegs;
 
 void fake_gpu_fail(void)
@@ -33,9 +33,14 @@ int ff_gpucrypto_host_failed(void) { return failed; }
 
 int ff_gpucrypto_host_probe(const struct espgpu_session_params *csp)
 {
+	int r;
+
 	if (failed)
 		return ESPGPU_ENXIO;
-	return espgpu_probesession(csp);
+	r = espgpu_probesession(csp);
+	/* the 3-slot SA table below is full: decline, as the real shim does on
+	 * espgpu_session_room() == 0 */
+	return r == ESPGPU_PROBE_HARDWARE && next_sid - nfreed >= 3 ? ESPGPU_ENOMEM : r;
 }
 
 int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_t *sid)
@@ -47,7 +52,11 @@ int ff_gpucrypto_host_newsession(const struct espgpu_session_params *csp, int32_
 	return next_sid > 3 ? ESPGPU_ENOMEM : ESPGPU_OK;     /* a 3-slot SA table */
 }
 
-void ff_gpucrypto_host_freesession(int32_t sid) { fake_freed_sid = sid; }
+void ff_gpucrypto_host_freesession(int32_t sid)
+{
+	fake_freed_sid = sid;
+	nfreed++;
+}
 
 static uint8_t byte_at(const struct espgpu_req *r, uint32_t off)
 {

@@ -83,7 +83,15 @@ int main(void)
 	csp.csp_ivlen = 12;
 	CHECK(kmock_newsession(&s3, &csp) == 0);
 	CHECK(kmock_newsession(&s4, &csp) == 0);
-	CHECK(kmock_newsession(&s2, &csp) == ENOMEM);      /* SA table full */
+	/* the SA table is full: the probe declines (ENOMEM), and with the
+	 * software driver present crypto_newsession selects it instead */
+	CHECK(kmock_newsession(&s2, &csp) == ENOMEM && s2 == NULL);
+	kmock_soft_enable(1);
+	CHECK(kmock_newsession(&s2, &csp) == 0 && crypto_ses2hid(s2) == KMOCK_SOFT_ID);
+	CHECK(st->soft_sessions == 1);
+	kmock_freesession(s2);
+	CHECK(st->soft_sessions == 0);
+	kmock_soft_enable(0);
 
 	/* four stage; the fifth hits a full staging area: ERESTART reaches the
 	 * framework, which queues it and blocks the driver; the sixth queues

@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     assert len(syms) >= 15
     for s in syms:
         assert hasattr(lib, s), "missing export %s" % s
-    assert lib.espgpu_abi_version() == 5
+    assert lib.espgpu_abi_version() == 6    # ABI 6: espgpu_session_room
 
 
 def test_struct_layouts():

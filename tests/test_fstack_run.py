@@ -171,6 +171,8 @@ def _run(exe, workload, tmp_path, fail=False):
     p = subprocess.run([exe, rq, rs] + (["--fail"] if fail else []), capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
     assert "fstack_crypto_run OK" in p.stdout
+    if not fail:                                     # host_main.c 4b: a full SA table -> cryptosoft
+        assert "the next went to cryptosoft" in p.stdout
     return FR.read_results(rs, [len(r["buf"]) for r in reqs], fail=fail)
 
 

@@ -571,6 +571,60 @@ def _req_view(kd, build, ses, esa, view):
 # GPU failure: every cryptop completes exactly once
 
 KMOCK_SOFT_ID, BSD_EIO, BSD_EAGAIN = 8, 5, 35
+def test_full_sa_table_sends_the_next_session_to_software(kd):
+    """kd_open's engine holds 64 SAs (espgpu_config.max_sessions).  The 65th
+    session is declined at probe (espgpu_session_room == 0): ENOMEM with no
+    software driver, and with one crypto_newsession selects it -- the SA is
+    never failed in CRYPTODEV_NEWSESSION (crypto.c:954-958).  A freed GPU
+    session's slot takes the next SA, whose requests decrypt as the oracle."""
+    from espgpu.esp import esp_input_crp
+    L = kd.L
+    L.kd_soft.argtypes = [C.c_void_p]
+    soft = (C.c_int * 4)()
+    rng = np.random.default_rng(6464)
+    hs = []
+    for _ in range(64):
+        e, h = kd.newsession(GcmSA(rng, 16).esp_sa())
+        assert e == 0
+        hs.append(h)
+    L.kd_soft(soft)
+    assert soft[0] == 0 and soft[2] == 64
+    sa = GcmSA(rng, 16)
+    esa = sa.esp_sa()
+    e, h = kd.newsession(esa)
+    assert e == 12 and not h                             # ENOMEM: the probe declined
+    L.kd_soft_enable(1)
+    e, hsw = kd.newsession(esa)
+    assert e == 0
+    L.kd_soft(soft)
+    assert soft[0] == 1 and soft[2] == 65                # on the software driver
+    kd.freesession(hs.pop(5))
+    e, ses = kd.newsession(esa)
+    assert e == 0
+    L.kd_soft(soft)
+    assert soft[0] == 1                                  # the freed GPU slot, not software
+    n = 24
+    plain, ct, descs, _ = build_records(rng, [sa], np.zeros(n, dtype=np.int64), rng.integers(1, 92, n) * 16)
+    ref = ct.copy()
+    _, ref_st = O.batch([sa.oracle], ref, descs["off4"], descs["len"], descs["sa"])
+    reqs, bufs_all = [], []
+    for i in range(n):
+        bufs = bytearray(_pkt(ct, descs, i))
+        r = kd.request(ses, esp_input_crp(_Fw(), ses, esa, bufs, 20), bufs)
+        assert kd.dispatch(r) == 0
+        reqs.append(r)
+        bufs_all.append(bufs)
+    assert kd.wait(reqs) == [0] * n
+    kd.free(reqs)
+    for i, bufs in enumerate(bufs_all):
+        o, Ln = int(descs["off4"][i]) * 4, int(descs["len"][i])
+        assert ref_st[i] == 0 and bytes(bufs[20 + 16:20 + Ln - 16]) == ref[o + 16:o + Ln - 16].tobytes(), i
+    for h in hs + [hsw, ses]:
+        kd.freesession(h)
+    L.kd_soft(soft)
+    assert soft[0] == 0 and soft[2] == 0
+
+
 FAULT_LAUNCH, FAULT_QUERY, FAULT_STUCK = 1, 2, 4     # set_tuning "fault" (include/espgpu.h)
 
 
