@@ -245,6 +245,8 @@ def main():
                     help="experiment: comma list of packet sizes drawn uniformly instead of the config's")
     ap.add_argument("--sa-runs", action="store_true",
                     help="experiment: lay each SA's records out back to back (placement probe)")
+    ap.add_argument("--planner", action="store_true",
+                    help="experiment: run single-SA batches through the device planner too (not grouped)")
     ap.add_argument("--dry-plan", action="store_true",
                     help="test aid: run the N-rank launch and each rank's packet plan on gloo/CPU, no GPU")
     ap.add_argument("--packets", type=int, default=0, help="with --dry-plan: packets per GPU override")
@@ -339,7 +341,9 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     arena = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
-    grouped = len(spis) == 1
+    grouped = len(spis) == 1 and not args.planner
+    if args.planner:
+        cfg["workload"] += " [device planner]"
     encrypt_batch(drv, arena, desc, n, status, grouped=grouped)     # build valid ESP records (untimed)
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0, "record generation failed"
