@@ -245,6 +245,8 @@ def main():
                     help="experiment: comma list of packet sizes drawn uniformly instead of the config's")
     ap.add_argument("--sa-runs", action="store_true",
                     help="experiment: lay each SA's records out back to back (placement probe)")
+    ap.add_argument("--sa-even", action="store_true",
+                    help="experiment: the same SAs and placement rule, but every SA gets the same record count")
     ap.add_argument("--planner", action="store_true",
                     help="experiment: run single-SA batches through the device planner too (not grouped)")
     ap.add_argument("--dry-plan", action="store_true",
@@ -303,6 +305,10 @@ def main():
         sizes = np.random.default_rng(0xE5B0000F + rank).choice(
             np.array([int(x) for x in args.sizes.split(",")]), len(sizes))
         cfg["workload"] += " [packet sizes overridden: %s]" % args.sizes
+    if args.sa_even:
+        nsa_here = len(spis)
+        sa_of = np.random.default_rng(0xE5B00010 + rank).permutation(np.arange(len(sa_of)) % nsa_here)
+        cfg["workload"] += " [equal record count per SA]"
     if args.sa_runs:
         order = np.argsort(sa_of, kind="stable")
         sa_of, sizes = sa_of[order], sizes[order]
